@@ -1,0 +1,46 @@
+import glob
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_ROOT = os.path.join(REPO, "mapf-marl_amd")
+for p in (REPO, PKG_ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+def load_fixture(name):
+    d = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    return {k: d[k] for k in d.files}
+
+
+def step_fixtures():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
+                  if not os.path.basename(p).startswith("primal"))
+
+
+def primal_fixtures():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "primal*.npz")))
+
+
+def fixture_rewards(fx):
+    """(step_reward, collide_reward) with the Python types the reference saw."""
+    sr = fx["meta_step_reward"].item()
+    cr = fx["meta_collide_reward"].item()
+    sr = int(sr) if bool(fx["meta_step_is_int"]) else float(sr)
+    cr = int(cr) if bool(fx["meta_collide_is_int"]) else float(cr)
+    return sr, cr
+
+
+@pytest.fixture
+def fixture_loader():
+    return load_fixture

@@ -1,0 +1,961 @@
+// mapfx.hip — MI355X (gfx950, CDNA4) batched MAPF gridworld step.
+//
+// One launch steps E independent envs of the reference's MAPF_GRID
+// (MARL-curve-main/src/envs/mapf_gridworld.py:85-141) and emits its
+// observations (:143-224), the marl_partial window (envs/marl_partial.py:323-342)
+// and the PRIMAL window (envs/mapf_primal.py:343-386).
+//
+// Execution model:
+//   * an env is owned by a lane group of L = pow2ceil(N) lanes (<= 256) of one
+//     workgroup; lane l owns agents l, l+L, ... (APL agents per lane);
+//     N = 16 puts 4 envs in a wavefront, 16 envs in a 256-thread workgroup;
+//   * the env's occupancy lives in LDS as a PADDED cell map: one byte per cell
+//     (u16 when N > 127) = obstacle flag (top bit) | agent count.  The border
+//     of P cells is "obstacle, 0 agents", which is exactly how the reference
+//     treats out-of-bounds cells for moves (:336-337), avail (:209-222) and the
+//     windows (marl_partial.py:335-337, mapf_primal.py:356-359), so no bounds
+//     test survives in the inner loops.  occ = count - flag.
+//   * per step: moves test the PRE-step map (quirk 1: an obstacle is passable
+//     while an agent stands on it), agent counts are then moved with LDS
+//     atomics, node collisions read the post-step count, edge collisions scan
+//     the env's agents only for agents that moved into a pre-occupied cell;
+//     rewards are folded in fp64 in agent order by one lane (quirk 4);
+//   * window observations are staged in LDS and leave as 16-byte stores.
+//
+// No MFMA: the step is integer gather/scatter + a short fp64 fold; HBM-bound.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <string>
+
+#include "mapfx.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__host__ __device__ inline int gen_action(uint64_t seed, int64_t env, int32_t t, int32_t agent) {
+  uint64_t k = seed ^ ((uint64_t)env * 0xD1B54A32D192ED03ull) ^
+               ((uint64_t)(uint32_t)t * 0xABC98388FB8FAC03ull) ^
+               ((uint64_t)(uint32_t)agent * 0x8CB92BA72F3D8DD7ull);
+  return (int)(splitmix64(k) % 5ull);
+}
+
+// x / d for 0 <= x < 2^32, 1 <= d < 2^16, with m = ceil(2^48 / d).
+__device__ inline int fastdiv(int x, uint64_t m) {
+  return (int)(((uint64_t)(uint32_t)x * m) >> 48);
+}
+
+// Launch geometry + env constants (uniform per launch).
+struct Geo {
+  int H, W, N, E;
+  long long env_offset;
+  int L, lshift, EPB, BT;
+  int P, pl, pitch, rows;  // padded LDS map: rows x pitch cells, interior at (P, pl)
+  int map_words;           // u32 words of one env's LDS map
+  int bits_words;          // u32 words of the bitmap actually used: ceil(H*W/32)
+  long long map_stride;    // bytes per env bitmap in global memory
+  int map_shared;
+  uint64_t m_wpr;          // fastdiv magic for words-per-padded-row
+  uint64_t m_W;            // fastdiv magic for W
+  uint64_t m_W4;           // fastdiv magic for W/4
+  int wpr;
+  // LDS regions (byte offsets from the dynamic LDS base)
+  int off_map, off_bits, off_oldc, off_newc, off_rc, off_goal, off_rew, off_flag, off_stage;
+  int map_env_bytes, bits_env_bytes, stage_env_bytes;
+  int window, wlen;        // marl_partial window w, 2*w*w
+  int psize;               // PRIMAL observation size s
+  int obs_mode;
+  int limit;
+  double step_rew, collide_rew;
+};
+
+struct Args {
+  int32_t* pos;
+  const int32_t* goal;
+  const int32_t* init_pos;
+  uint8_t* done;
+  int32_t* t;
+  int32_t* steps;
+  const uint8_t* bits;
+  const void* actions;
+  int act_dtype;
+  int use_rng;
+  uint64_t seed;
+  int t0;
+  int T;
+  int autoreset;
+  int do_step;
+  double* reward;
+  float* reward_f32;
+  uint8_t* term;
+  uint8_t* node;
+  uint8_t* edge;
+  uint8_t* avail;
+  void* obs_full;
+  void* obs_window;
+  uint8_t* obs_primal;
+  double* primal_vec;
+  int32_t* traj_pos;
+  uint8_t* traj_done;
+  int32_t* traj_t;
+  int32_t* err;
+  const double* pow_lut;
+};
+
+template <typename CellT>
+struct CellTraits;
+template <>
+struct CellTraits<uint8_t> {
+  static constexpr uint32_t OE = 0x80u;        // obstacle flag, 0 agents
+  static constexpr uint32_t CNT = 0x7Fu;
+  static constexpr uint32_t OE_WORD = 0x80808080u;
+  static constexpr int PER_WORD_SHIFT = 2;     // 4 cells per u32
+  __device__ static inline uint32_t inc(int cell) { return 1u << ((cell & 3) * 8); }
+};
+template <>
+struct CellTraits<uint16_t> {
+  static constexpr uint32_t OE = 0x8000u;
+  static constexpr uint32_t CNT = 0x7FFFu;
+  static constexpr uint32_t OE_WORD = 0x80008000u;
+  static constexpr int PER_WORD_SHIFT = 1;     // 2 cells per u32
+  __device__ static inline uint32_t inc(int cell) { return 1u << ((cell & 1) * 16); }
+};
+
+// (row, col) deltas of actions 0..3 (envs/mapf_gridworld.py:323-330)
+__device__ inline int act_dr(int a) { return a == 0 ? -1 : (a == 1 ? 1 : 0); }
+__device__ inline int act_dc(int a) { return a == 2 ? -1 : (a == 3 ? 1 : 0); }
+
+__device__ inline int load_action(const void* p, int dtype, long long idx) {
+  if (dtype == MAPFX_I8) return (int)((const int8_t*)p)[idx];
+  if (dtype == MAPFX_I32) {
+    return ((const int32_t*)p)[idx];
+  }
+  long long v = ((const int64_t*)p)[idx];
+  return (v < -1 || v > 5) ? -1 : (int)v;  // any out-of-range value is invalid
+}
+
+// Bit (r*W + c) of the env's bitmap staged in LDS.
+__device__ inline uint32_t map_bit(const uint32_t* bits, int idx) {
+  return (bits[idx >> 5] >> (idx & 31)) & 1u;
+}
+
+// Build the padded occupancy map of one env from its LDS bitmap (no agents).
+template <typename CellT>
+__device__ inline void fill_map(const Geo& g, uint32_t* map32, const uint32_t* bits, int lane) {
+  using CT = CellTraits<CellT>;
+  constexpr int CPW = 1 << CT::PER_WORD_SHIFT;  // cells per word
+  for (int wi = lane; wi < g.map_words; wi += g.L) {
+    const int pr = fastdiv(wi, g.m_wpr);
+    const int pw = wi - pr * g.wpr;
+    const int r = pr - g.P;
+    uint32_t word;
+    if (r < 0 || r >= g.H) {
+      word = CT::OE_WORD;
+    } else {
+      word = 0;
+      const int c0 = pw * CPW - g.pl;
+#pragma unroll
+      for (int j = 0; j < CPW; ++j) {
+        const int c = c0 + j;
+        uint32_t ob = 1u;
+        if (c >= 0 && c < g.W) ob = map_bit(bits, r * g.W + c);
+        word |= (ob ? CT::OE : 0u) << (j * (32 / CPW));
+      }
+    }
+    map32[wi] = word;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The step kernel: T fused steps (T = 1 for mapfx_step; do_step = 0 observes).
+// ---------------------------------------------------------------------------
+template <typename CellT, int APL>
+__global__ void __launch_bounds__(256) mapf_step_kernel(Geo g, Args a) {
+  using CT = CellTraits<CellT>;
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int tid = threadIdx.x;
+  const int slot = tid >> g.lshift;
+  const int lane = tid & (g.L - 1);
+  const int env0 = blockIdx.x * g.EPB;
+  const int env = env0 + slot;
+  const bool env_ok = env < g.E;
+  const int N = g.N;
+
+  uint32_t* map32 = (uint32_t*)(lds + g.off_map + slot * g.map_env_bytes);
+  CellT* map = (CellT*)map32;
+  uint32_t* bitsL = (uint32_t*)(lds + g.off_bits + slot * g.bits_env_bytes);
+  int* oldc = (int*)(lds + g.off_oldc) + slot * N;
+  int* newc = (int*)(lds + g.off_newc) + slot * N;
+  int* rcs = (int*)(lds + g.off_rc) + slot * N;
+  int* gls = (int*)(lds + g.off_goal) + slot * N;
+  double* rew = (double*)(lds + g.off_rew) + slot * N;
+  int* flag = (int*)(lds + g.off_flag) + slot * 8;  // [parity*4 + {alldone, bad}]
+  unsigned char* stage_blk = lds + g.off_stage;
+
+  // ---- per-lane agent state (registers) ----
+  int r[APL], c[APL], gr[APL], gc[APL], st[APL];
+  bool dn[APL], has[APL];
+#pragma unroll
+  for (int k = 0; k < APL; ++k) {
+    const int ag = lane + k * g.L;
+    has[k] = env_ok && ag < N;
+    r[k] = c[k] = gr[k] = gc[k] = st[k] = 0;
+    dn[k] = false;
+    if (has[k]) {
+      const long long i = (long long)env * N + ag;
+      const int2 p = ((const int2*)a.pos)[i];
+      const int2 q = ((const int2*)a.goal)[i];
+      r[k] = p.x;
+      c[k] = p.y;
+      gr[k] = q.x;
+      gc[k] = q.y;
+      dn[k] = a.done[i] != 0;
+      if (a.steps) st[k] = a.steps[i];
+      gls[ag] = (q.x << 16) | (q.y & 0xFFFF);
+    }
+  }
+  int tcur = env_ok ? a.t[env] : 0;
+
+  // ---- stage the bitmap, build the padded map, add the agents ----
+  if (env_ok) {
+    const uint32_t* src =
+        (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)env * g.map_stride));
+    for (int w = lane; w < g.bits_words; w += g.L) bitsL[w] = src[w];
+  }
+  for (int i = lane; i < 8; i += g.L) flag[i] = (i & 3) == 0 ? 1 : 0;  // alldone = 1, bad = 0
+  __syncthreads();
+  fill_map<CellT>(g, map32, bitsL, lane);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < APL; ++k) {
+    if (has[k]) {
+      const int cell = (r[k] + g.P) * g.pitch + c[k] + g.pl;
+      atomicAdd(&map32[cell >> CT::PER_WORD_SHIFT], CT::inc(cell));
+    }
+  }
+  __syncthreads();
+
+  const int wlen = g.wlen;
+  const int es = (int)sizeof(CellT);  // obs element size == cell size
+  const long long Elong = g.E;
+
+  for (int s = 0; s < a.T; ++s) {
+    int* fl = flag + (s & 1) * 4;
+    // ================= P0: move decision on the PRE-step map =================
+    int oc[APL], nc[APL], act[APL], pre[APL];
+    bool moved[APL], envc[APL];
+#pragma unroll
+    for (int k = 0; k < APL; ++k) {
+      const int ag = lane + k * g.L;
+      oc[k] = (r[k] + g.P) * g.pitch + c[k] + g.pl;
+      nc[k] = oc[k];
+      moved[k] = envc[k] = false;
+      pre[k] = 0;
+      act[k] = 4;
+      if (has[k] && a.do_step) {
+        int av;
+        if (a.use_rng)
+          av = gen_action(a.seed, g.env_offset + env, a.t0 + s, ag);
+        else
+          av = load_action(a.actions, a.act_dtype, ((long long)s * Elong + env) * N + ag);
+        if (av < 0 || av > 4) {
+          atomicOr(&fl[1], 1);
+          av = 4;
+        }
+        act[k] = av;
+        if (!dn[k] && av != 4) {  // __agent_step :319-342
+          const int cand =
+              oc[k] + (av == 0 ? -g.pitch : (av == 1 ? g.pitch : (av == 2 ? -1 : 1)));
+          const uint32_t v = map[cand];
+          if (v == CT::OE) {
+            envc[k] = true;       // out of bounds or free-standing obstacle
+          } else {
+            nc[k] = cand;
+            moved[k] = true;
+            pre[k] = (int)(v & CT::CNT);
+          }
+        }
+        oldc[ag] = oc[k];
+        newc[ag] = nc[k];
+      }
+    }
+    __syncthreads();  // B1: every pre-step map read is done
+    // ================= P1: move the agent counts =================
+    const bool skip = (fl[1] != 0) || !a.do_step;
+#pragma unroll
+    for (int k = 0; k < APL; ++k) {
+      if (!has[k]) continue;
+      const int ag = lane + k * g.L;
+      if (skip) {
+        nc[k] = oc[k];
+        moved[k] = envc[k] = false;
+        newc[ag] = oc[k];
+      } else if (moved[k]) {
+        atomicSub(&map32[oc[k] >> CT::PER_WORD_SHIFT], CT::inc(oc[k]));
+        atomicAdd(&map32[nc[k] >> CT::PER_WORD_SHIFT], CT::inc(nc[k]));
+        r[k] += act_dr(act[k]);
+        c[k] += act_dc(act[k]);
+      }
+      rcs[ag] = (r[k] << 16) | (c[k] & 0xFFFF);
+    }
+    if (a.do_step && !skip && env_ok) ++tcur;
+    __syncthreads();  // B2: post-step map complete
+    // ================= P2: collisions, rewards, avail, observations =================
+    const long long slotE = a.T > 1 ? (long long)s * Elong : 0;  // trajectory slot offset (envs)
+#pragma unroll
+    for (int k = 0; k < APL; ++k) {
+      if (!has[k]) continue;
+      const int ag = lane + k * g.L;
+      const long long ai = (slotE + env) * N + ag;  // output agent index
+      int node = 0, edge = 0;
+      if (a.do_step && !skip) {
+        node = ((uint32_t)map[nc[k]] & CT::CNT) > 1u ? 1 : 0;  // :344-362
+        if (moved[k] && pre[k] > 0) {                           // :364-383
+          for (int j = 0; j < N; ++j)
+            edge += (oldc[j] == nc[k]) & (newc[j] == oc[k]);
+        }
+        double rr = 0.0;  // :94-130, exact fp64 op order
+        if (!dn[k]) {
+          if (envc[k]) rr = rr + g.collide_rew;
+          rr = rr + g.step_rew;
+          ++st[k];
+        }
+        rr = rr + g.collide_rew * (double)node;
+        rr = rr + g.collide_rew * (double)edge;
+        rew[ag] = rr;
+        if (r[k] == gr[k] && c[k] == gc[k]) dn[k] = true;  // :112-114
+        if (tcur >= g.limit) dn[k] = true;                   // :116-117
+      } else if (a.do_step) {
+        rew[ag] = 0.0;
+      }
+      if (!dn[k]) atomicAnd(&fl[0], 0);
+      if (a.do_step) {
+        if (a.node) a.node[ai] = (uint8_t)node;
+        if (a.edge) a.edge[ai] = (uint8_t)(edge > 255 ? 255 : edge);
+      }
+      if (a.traj_pos) ((int2*)a.traj_pos)[ai] = make_int2(r[k], c[k]);
+      if (a.traj_done) a.traj_done[ai] = dn[k] ? 1 : 0;
+      if (a.avail) {  // :203-224 on the post-step map
+        const int cc = nc[k];
+        uint32_t m = 16u;
+        m |= ((uint32_t)map[cc - g.pitch] != CT::OE) ? 1u : 0u;
+        m |= ((uint32_t)map[cc + g.pitch] != CT::OE) ? 2u : 0u;
+        m |= ((uint32_t)map[cc - 1] != CT::OE) ? 4u : 0u;
+        m |= ((uint32_t)map[cc + 1] != CT::OE) ? 8u : 0u;
+        a.avail[ai] = (uint8_t)m;
+      }
+      if (a.obs_window) {  // marl_partial.py:323-342 -> LDS staging
+        const int w = g.window, h = w >> 1;
+        unsigned char* dst = stage_blk + (size_t)(slot * N + ag) * wlen * es;
+        const int base = nc[k] - h * g.pitch - h;
+        for (int y = 0; y < w; ++y) {
+          for (int x = 0; x < w; ++x) {
+            const uint32_t v = map[base + y * g.pitch + x];
+            const int cnt = (int)(v & CT::CNT);
+            const int ob = (v & CT::OE) ? 1 : 0;
+            const int occ = cnt - ob;
+            const int o0 = (occ == -1) ? 1 : 0;
+            const int o1 = occ > 0 ? occ : 0;
+            if (es == 1) {
+              dst[y * w + x] = (unsigned char)o0;
+              dst[w * w + y * w + x] = (unsigned char)o1;
+            } else {
+              ((int16_t*)dst)[y * w + x] = (int16_t)o0;
+              ((int16_t*)dst)[w * w + y * w + x] = (int16_t)o1;
+            }
+          }
+        }
+      }
+    }
+    if (a.obs_primal || a.primal_vec) {  // rcs[] (written in P1) is visible since B2
+#pragma unroll
+      for (int k = 0; k < APL; ++k) {
+        if (!has[k]) continue;
+        const int ag = lane + k * g.L;
+        const long long ai = (slotE + env) * N + ag;
+        const int S = g.psize, h = S >> 1;
+        const int tr = r[k] - h, tc = c[k] - h;
+        if (a.obs_primal) {
+          // goals channel: goals of visible other agents clamped into the window
+          uint64_t gm0 = 0, gm1 = 0;
+          for (int j = 0; j < N; ++j) {
+            if (j == ag) continue;
+            const int rc = rcs[j];
+            const int jr = rc >> 16, jc = (int)(int16_t)(rc & 0xFFFF);
+            if (jr < tr || jr >= tr + S || jc < tc || jc >= tc + S) continue;
+            const int gg = gls[j];
+            int xr = gg >> 16, xc = (int)(int16_t)(gg & 0xFFFF);
+            xr = max(tr, min(tr + S - 1, xr));
+            xc = max(tc, min(tc + S - 1, xc));
+            const int q = (xr - tr) * S + (xc - tc);
+            if (q < 64) gm0 |= 1ull << q; else gm1 |= 1ull << (q - 64);
+          }
+          uint8_t* out = a.obs_primal + ai * 4 * S * S;
+          const int base = (tr + g.P) * g.pitch + tc + g.pl;
+          for (int y = 0; y < S; ++y) {
+            for (int x = 0; x < S; ++x) {
+              const int q = y * S + x;
+              const uint32_t v = map[base + y * g.pitch + x];
+              out[q] = (v & CT::CNT) ? 1 : 0;                                  // poss
+              out[S * S + q] = (tr + y == gr[k] && tc + x == gc[k]) ? 1 : 0;   // goal
+              out[2 * S * S + q] =
+                  (uint8_t)(((q < 64 ? gm0 >> q : gm1 >> (q - 64))) & 1ull);   // goals
+              out[3 * S * S + q] = (v == CT::OE) ? 1 : 0;                      // obs
+            }
+          }
+        }
+        if (a.primal_vec) {  // mapf_primal.py:380-386; mag via host libm pow LUT
+          const int dx = gr[k] - r[k], dy = gc[k] - c[k];
+          const double mag = a.pow_lut[dx * dx + dy * dy];
+          double vx = (double)dx, vy = (double)dy;
+          if (mag != 0.0) {
+            vx = vx / mag;
+            vy = vy / mag;
+          }
+          double* o = a.primal_vec + ai * 3;
+          o[0] = vx;
+          o[1] = vy;
+          o[2] = mag;
+        }
+      }
+    }
+    if (a.obs_full && env_ok) {  // :143-192: row-major occ = count - flag
+      const long long HW = (long long)g.H * g.W;
+      unsigned char* outb = (unsigned char*)a.obs_full + (slotE + env) * HW * es;
+      if (es == 1 && (g.W & 3) == 0) {
+        const int wpr_out = g.W >> 2;
+        const int nwords = g.H * wpr_out;
+        for (int i = lane; i < nwords; i += g.L) {
+          const int rr_ = fastdiv(i, g.m_W4);
+          const int cw = i - rr_ * wpr_out;
+          const uint32_t v = map32[((rr_ + g.P) * g.pitch + g.pl) / 4 + cw];
+          const uint32_t f = (v >> 7) & 0x01010101u;
+          const uint32_t o = (((v & 0x7F7F7F7Fu) | 0x80808080u) - f) ^ 0x80808080u;
+          ((uint32_t*)outb)[i] = o;
+        }
+      } else {
+        for (int i = lane; i < (int)HW; i += g.L) {
+          const int rr_ = fastdiv(i, g.m_W);
+          const int cc_ = i - rr_ * g.W;
+          const uint32_t v = map[(rr_ + g.P) * g.pitch + cc_ + g.pl];
+          const int occ = (int)(v & CT::CNT) - ((v & CT::OE) ? 1 : 0);
+          if (es == 1)
+            ((int8_t*)outb)[i] = (int8_t)occ;
+          else
+            ((int16_t*)outb)[i] = (int16_t)occ;
+        }
+      }
+    }
+    __syncthreads();  // B3: rew[], flags and staging complete
+    // ================= P3: fold, term, staging copy-out, autoreset =================
+    const bool alldone = fl[0] != 0;
+    if (env_ok && lane == 0) {
+      if (a.do_step) {
+        if (fl[1] && a.err) atomicCAS(a.err, 0, env + 1);
+        double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
+        for (int j = 0; j < N; ++j) R = R + rew[j];
+        if (a.reward) a.reward[slotE + env] = R;
+        if (a.reward_f32) a.reward_f32[slotE + env] = (float)R;
+      }
+      if (a.term) a.term[slotE + env] = alldone ? 1 : 0;
+      if (a.traj_t) a.traj_t[slotE + env] = tcur;
+      int* nf = flag + ((s + 1) & 1) * 4;
+      nf[0] = 1;
+      nf[1] = 0;
+    }
+    if (a.obs_window) {
+      const int nenv = min(g.EPB, g.E - env0);
+      const long long bytes = (long long)nenv * N * wlen * es;
+      unsigned char* dst =
+          (unsigned char*)a.obs_window + ((slotE + env0) * (long long)N * wlen) * es;
+      if ((((uintptr_t)dst) & 15) == 0 && (bytes & 15) == 0) {
+        const uint4* s4 = (const uint4*)stage_blk;
+        uint4* d4 = (uint4*)dst;
+        for (long long i = tid; i < (bytes >> 4); i += g.BT) d4[i] = s4[i];
+      } else if ((((uintptr_t)dst) & 3) == 0 && (bytes & 3) == 0) {
+        const uint32_t* s4 = (const uint32_t*)stage_blk;
+        uint32_t* d4 = (uint32_t*)dst;
+        for (long long i = tid; i < (bytes >> 2); i += g.BT) d4[i] = s4[i];
+      } else {
+        for (long long i = tid; i < bytes; i += g.BT) dst[i] = stage_blk[i];
+      }
+    }
+    // optional autoreset of envs whose agents are all done
+#pragma unroll
+    for (int k = 0; k < APL; ++k) {
+      if (!has[k]) continue;
+      const int ag = lane + k * g.L;
+      const long long i = (long long)env * N + ag;
+      if (a.autoreset && alldone && a.do_step) {
+        const int2 p = ((const int2*)a.init_pos)[i];
+        const int ocell = (r[k] + g.P) * g.pitch + c[k] + g.pl;
+        const int ncell = (p.x + g.P) * g.pitch + p.y + g.pl;
+        atomicSub(&map32[ocell >> CT::PER_WORD_SHIFT], CT::inc(ocell));
+        atomicAdd(&map32[ncell >> CT::PER_WORD_SHIFT], CT::inc(ncell));
+        r[k] = p.x;
+        c[k] = p.y;
+        dn[k] = false;
+        st[k] = 0;
+      }
+    }
+    if (a.autoreset && alldone && a.do_step) tcur = 0;
+    if (s + 1 < a.T) __syncthreads();  // B4: map / staging reuse by the next step
+  }
+
+  // ---- write back the env state ----
+#pragma unroll
+  for (int k = 0; k < APL; ++k) {
+    if (!has[k]) continue;
+    const int ag = lane + k * g.L;
+    const long long i = (long long)env * N + ag;
+    ((int2*)a.pos)[i] = make_int2(r[k], c[k]);
+    a.done[i] = dn[k] ? 1 : 0;
+    if (a.steps) a.steps[i] = st[k];
+  }
+  if (env_ok && lane == 0) a.t[env] = tcur;
+}
+
+__global__ void reset_kernel(int E, int N, int32_t* pos, const int32_t* init_pos, uint8_t* done,
+                             int32_t* t, int32_t* steps, const uint8_t* mask) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)E * N) return;
+  const long long e = i / N;
+  if (mask && !mask[e]) return;
+  ((int2*)pos)[i] = ((const int2*)init_pos)[i];
+  done[i] = 0;
+  if (steps) steps[i] = 0;
+  if (i % N == 0) t[e] = 0;
+}
+
+__global__ void gen_actions_kernel(long long total, int E, int N, long long env_offset,
+                                   uint64_t seed, int t0, int8_t* out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const long long en = (long long)E * N;
+  const int tt = (int)(i / en);
+  const long long rem = i - (long long)tt * en;
+  const long long e = rem / N;
+  const int ag = (int)(rem - e * N);
+  out[i] = (int8_t)gen_action(seed, env_offset + e, t0 + tt, ag);
+}
+
+int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+uint64_t magic48(int d) { return ((1ull << 48) + (uint64_t)d - 1) / (uint64_t)d; }
+
+}  // namespace
+
+struct mapfx_t {
+  mapfx_cfg cfg;
+  Geo geo;
+  int cell_bytes;
+  int APL;
+  double* pow_lut;  // device
+  int lut_len;
+  int device;
+};
+
+namespace {
+
+using KernelFn = void (*)(Geo, Args);
+
+KernelFn pick_kernel(int cell_bytes, int apl) {
+  if (cell_bytes == 1) {
+    if (apl == 1) return mapf_step_kernel<uint8_t, 1>;
+    if (apl == 2) return mapf_step_kernel<uint8_t, 2>;
+    return mapf_step_kernel<uint8_t, 4>;
+  }
+  if (apl == 1) return mapf_step_kernel<uint16_t, 1>;
+  if (apl == 2) return mapf_step_kernel<uint16_t, 2>;
+  return mapf_step_kernel<uint16_t, 4>;
+}
+
+int check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) return set_error(MAPFX_EHIP, "%s: %s", what, hipGetErrorString(e));
+  return MAPFX_OK;
+}
+
+int launch(mapfx_t* h, Args& a, hipStream_t stream) {
+  const Geo& g = h->geo;
+  if (g.E == 0) return MAPFX_OK;
+  KernelFn fn = pick_kernel(h->cell_bytes, h->APL);
+  const int blocks = (g.E + g.EPB - 1) / g.EPB;
+  const int lds = g.off_stage + g.EPB * g.stage_env_bytes;
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, g, a);
+  return check_hip(hipGetLastError(), "mapf_step_kernel launch");
+}
+
+void fill_state_args(Args& a, const mapfx_state* st) {
+  a.pos = st->pos;
+  a.goal = st->goal;
+  a.init_pos = st->init_pos;
+  a.done = st->done;
+  a.t = st->t;
+  a.steps = st->steps;
+  a.bits = st->map_bits;
+}
+
+void fill_out_args(Args& a, const mapfx_out* o) {
+  if (!o) return;
+  a.reward = o->reward;
+  a.reward_f32 = o->reward_f32;
+  a.term = o->term;
+  a.node = o->node;
+  a.edge = o->edge;
+  a.avail = o->avail;
+  a.obs_full = o->obs_full;
+  a.obs_window = o->obs_window;
+  a.obs_primal = o->obs_primal;
+  a.primal_vec = o->primal_vec;
+  a.traj_pos = o->traj_pos;
+  a.traj_done = o->traj_done;
+  a.traj_t = o->traj_t;
+  a.err = o->err;
+}
+
+int check_state(const mapfx_t* h, const mapfx_state* st, bool need_init) {
+  if (!st || !st->pos || !st->goal || !st->done || !st->t || !st->map_bits)
+    return set_error(MAPFX_EINVAL, "state: pos/goal/done/t/map_bits must be non-NULL");
+  if (need_init && !st->init_pos) return set_error(MAPFX_EINVAL, "state: init_pos is NULL");
+  (void)h;
+  return MAPFX_OK;
+}
+
+int check_out(const mapfx_t* h, const mapfx_out* o) {
+  if (!o) return MAPFX_OK;
+  const int m = h->cfg.obs_mode;
+  if (o->obs_full && !(m & MAPFX_OBS_FULL))
+    return set_error(MAPFX_EINVAL, "obs_full requested but MAPFX_OBS_FULL not in cfg.obs_mode");
+  if (o->obs_window && !(m & MAPFX_OBS_WINDOW))
+    return set_error(MAPFX_EINVAL, "obs_window requested but MAPFX_OBS_WINDOW not in cfg.obs_mode");
+  if ((o->obs_primal || o->primal_vec) && !(m & MAPFX_OBS_PRIMAL))
+    return set_error(MAPFX_EINVAL, "PRIMAL obs requested but MAPFX_OBS_PRIMAL not in cfg.obs_mode");
+  return MAPFX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mapfx_abi_version(void) { return MAPFX_ABI_VERSION; }
+
+const char* mapfx_last_error(void) { return g_last_error.c_str(); }
+
+int64_t mapfx_map_stride(int32_t H, int32_t W) {
+  const int64_t bytes = ((int64_t)H * W + 7) / 8;
+  return (bytes + 15) / 16 * 16;
+}
+
+int32_t mapfx_obs_elem_size(int32_t n_agents) { return n_agents <= 127 ? 1 : 2; }
+
+int32_t mapfx_action(uint64_t seed, int64_t env, int32_t t, int32_t agent) {
+  return gen_action(seed, env, t, agent);
+}
+
+int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
+  if (!cfg || !out_handle) return set_error(MAPFX_EINVAL, "NULL cfg/out_handle");
+  *out_handle = nullptr;
+  const mapfx_cfg& c = *cfg;
+  if (c.H < 1 || c.W < 1 || c.H > 4096 || c.W > 4096)
+    return set_error(MAPFX_EINVAL, "grid %dx%d out of range", c.H, c.W);
+  if (c.n_agents < 1 || c.n_agents > 1024)
+    return set_error(MAPFX_EINVAL, "n_agents %d not in 1..1024", c.n_agents);
+  if (c.n_envs < 0) return set_error(MAPFX_EINVAL, "n_envs < 0");
+  if ((c.obs_mode & MAPFX_OBS_WINDOW) && (c.window < 1 || c.window > 63))
+    return set_error(MAPFX_EINVAL, "window %d not in 1..63", c.window);
+  if ((c.obs_mode & MAPFX_OBS_PRIMAL) && (c.primal_size < 1 || c.primal_size > 11))
+    return set_error(MAPFX_EINVAL, "primal_size %d not in 1..11", c.primal_size);
+  if (c.H >= 32768 || c.W >= 32768) return set_error(MAPFX_EINVAL, "grid too large");
+
+  mapfx_t* h = new (std::nothrow) mapfx_t();
+  if (!h) return set_error(MAPFX_ENOMEM, "host allocation failed");
+  h->cfg = c;
+  h->pow_lut = nullptr;
+  h->lut_len = 0;
+  if (hipGetDevice(&h->device) != hipSuccess) h->device = 0;
+
+  Geo& g = h->geo;
+  memset(&g, 0, sizeof(g));
+  const int N = c.n_agents;
+  const int es = mapfx_obs_elem_size(N);
+  h->cell_bytes = es;
+  int L = 1;
+  while (L < N && L < 256) L <<= 1;
+  int lshift = 0;
+  while ((1 << lshift) < L) ++lshift;
+  const int APL = (N + L - 1) / L;
+  h->APL = APL <= 1 ? 1 : (APL <= 2 ? 2 : 4);
+
+  int P = 1;
+  if (c.obs_mode & MAPFX_OBS_WINDOW) {
+    P = std::max(P, c.window / 2);
+    P = std::max(P, c.window - 1 - c.window / 2);
+  }
+  if (c.obs_mode & MAPFX_OBS_PRIMAL) {
+    P = std::max(P, c.primal_size / 2);
+    P = std::max(P, c.primal_size - 1 - c.primal_size / 2);
+  }
+  const int cpw = 4 / es;  // cells per u32 word
+  const int pl = round_up(P, cpw);
+  const int pitch = round_up(pl + c.W + P, cpw);
+  const int rows = c.H + 2 * P;
+
+  g.H = c.H;
+  g.W = c.W;
+  g.N = N;
+  g.E = c.n_envs;
+  g.env_offset = c.env_offset;
+  g.L = L;
+  g.lshift = lshift;
+  g.P = P;
+  g.pl = pl;
+  g.pitch = pitch;
+  g.rows = rows;
+  g.wpr = pitch / cpw;
+  g.map_words = rows * g.wpr;
+  g.m_wpr = magic48(g.wpr);
+  g.m_W = magic48(c.W);
+  g.m_W4 = magic48(std::max(1, c.W / 4));
+  g.bits_words = (int)(((int64_t)c.H * c.W + 31) / 32);
+  g.map_stride = mapfx_map_stride(c.H, c.W);
+  g.map_shared = c.map_shared ? 1 : 0;
+  g.map_env_bytes = round_up(g.map_words * 4, 16);
+  g.bits_env_bytes = round_up(g.bits_words * 4, 16);
+  g.window = c.window;
+  g.wlen = 2 * c.window * c.window;
+  g.psize = c.primal_size;
+  g.obs_mode = c.obs_mode;
+  g.limit = c.episode_limit;
+  g.step_rew = c.step_reward;
+  g.collide_rew = c.collide_reward;
+  g.stage_env_bytes = (c.obs_mode & MAPFX_OBS_WINDOW) ? N * g.wlen * es : 0;
+
+  if ((int64_t)c.H * c.W >= (1ll << 31) / 8 || g.map_words >= (1 << 30)) {
+    delete h;
+    return set_error(MAPFX_EINVAL, "grid too large");
+  }
+
+  auto lds_for = [&](int epb) {
+    int off = 0;
+    off += epb * g.map_env_bytes;
+    off += epb * g.bits_env_bytes;
+    off += 4 * round_up(epb * N * 4, 16);  // oldc, newc, rc, goal
+    off += round_up(epb * N * 8, 16);      // rew
+    off += round_up(epb * 8 * 4, 16);      // flags
+    off += epb * g.stage_env_bytes;
+    return off;
+  };
+  int EPB = 256 / L;
+  const int LDS_TARGET = 48 * 1024;
+  const int LDS_MAX = 160 * 1024;
+  while (EPB > 1 && lds_for(EPB) > LDS_TARGET) --EPB;
+  if (lds_for(EPB) > LDS_MAX) {
+    delete h;
+    return set_error(MAPFX_EINVAL, "one env needs %d B of LDS (> %d)", lds_for(1), LDS_MAX);
+  }
+  g.EPB = EPB;
+  g.BT = EPB * L;
+  int off = 0;
+  g.off_map = off;
+  off += EPB * g.map_env_bytes;
+  g.off_bits = off;
+  off += EPB * g.bits_env_bytes;
+  g.off_oldc = off;
+  off += round_up(EPB * N * 4, 16);
+  g.off_newc = off;
+  off += round_up(EPB * N * 4, 16);
+  g.off_rc = off;
+  off += round_up(EPB * N * 4, 16);
+  g.off_goal = off;
+  off += round_up(EPB * N * 4, 16);
+  g.off_rew = off;
+  off += round_up(EPB * N * 8, 16);
+  g.off_flag = off;
+  off += round_up(EPB * 8 * 4, 16);
+  g.off_stage = off;
+
+  const int lds_total = g.off_stage + EPB * g.stage_env_bytes;
+  if (lds_total > 64 * 1024) {
+    KernelFn fn = pick_kernel(es, h->APL);
+    hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       lds_total);
+    if (e != hipSuccess) {
+      delete h;
+      return set_error(MAPFX_EHIP, "hipFuncSetAttribute(LDS=%d): %s", lds_total,
+                       hipGetErrorString(e));
+    }
+  }
+
+  if (c.obs_mode & MAPFX_OBS_PRIMAL) {
+    // mag = (dx**2 + dy**2) ** .5 is libm pow, not sqrt (mapf_primal.py:382, quirk 8):
+    // tabulate it on the host with the same libm the reference's CPython calls.
+    const int n = (c.H - 1) * (c.H - 1) + (c.W - 1) * (c.W - 1) + 1;
+    double* lut = (double*)malloc(sizeof(double) * n);
+    if (!lut) {
+      delete h;
+      return set_error(MAPFX_ENOMEM, "host LUT allocation failed");
+    }
+    for (int i = 0; i < n; ++i) lut[i] = pow((double)i, 0.5);
+    hipError_t e = hipMalloc((void**)&h->pow_lut, sizeof(double) * n);
+    if (e == hipSuccess) e = hipMemcpy(h->pow_lut, lut, sizeof(double) * n, hipMemcpyHostToDevice);
+    free(lut);
+    if (e != hipSuccess) {
+      if (h->pow_lut) (void)hipFree(h->pow_lut);
+      delete h;
+      return set_error(MAPFX_ENOMEM, "pow LUT: %s", hipGetErrorString(e));
+    }
+    h->lut_len = n;
+  }
+  *out_handle = h;
+  return MAPFX_OK;
+}
+
+void mapfx_destroy(mapfx_t* h) {
+  if (!h) return;
+  if (h->pow_lut) (void)hipFree(h->pow_lut);
+  delete h;
+}
+
+int mapfx_query(const mapfx_t* h, mapfx_info* info) {
+  if (!h || !info) return set_error(MAPFX_EINVAL, "NULL handle/info");
+  const Geo& g = h->geo;
+  info->lanes_per_env = g.L;
+  info->agents_per_lane = (g.N + g.L - 1) / g.L;
+  info->envs_per_block = g.EPB;
+  info->block_threads = g.BT;
+  info->lds_bytes = g.off_stage + g.EPB * g.stage_env_bytes;
+  info->cell_bytes = h->cell_bytes;
+  info->pad = g.P;
+  return MAPFX_OK;
+}
+
+int mapfx_reset(mapfx_t* h, const mapfx_state* st, const uint8_t* env_mask, const mapfx_out* out,
+                void* stream) {
+  if (!h) return set_error(MAPFX_EINVAL, "NULL handle");
+  int rc = check_state(h, st, true);
+  if (rc) return rc;
+  if ((rc = check_out(h, out))) return rc;
+  const Geo& g = h->geo;
+  const long long total = (long long)g.E * g.N;
+  if (total > 0) {
+    const int bt = 256;
+    hipLaunchKernelGGL(reset_kernel, dim3((unsigned)((total + bt - 1) / bt)), dim3(bt), 0,
+                       (hipStream_t)stream, g.E, g.N, st->pos, st->init_pos, st->done, st->t,
+                       st->steps, env_mask);
+    if ((rc = check_hip(hipGetLastError(), "reset_kernel launch"))) return rc;
+  }
+  if (out) return mapfx_observe(h, st, out, stream);
+  return MAPFX_OK;
+}
+
+int mapfx_observe(mapfx_t* h, const mapfx_state* st, const mapfx_out* out, void* stream) {
+  if (!h) return set_error(MAPFX_EINVAL, "NULL handle");
+  int rc = check_state(h, st, false);
+  if (rc) return rc;
+  if ((rc = check_out(h, out))) return rc;
+  if ((out && (out->obs_primal || out->primal_vec)) && !h->pow_lut)
+    return set_error(MAPFX_EINVAL, "PRIMAL LUT missing");
+  Args a;
+  memset(&a, 0, sizeof(a));
+  fill_state_args(a, st);
+  if (out) {
+    a.term = out->term;
+    a.avail = out->avail;
+    a.obs_full = out->obs_full;
+    a.obs_window = out->obs_window;
+    a.obs_primal = out->obs_primal;
+    a.primal_vec = out->primal_vec;
+  }
+  a.T = 1;
+  a.do_step = 0;
+  a.pow_lut = h->pow_lut;
+  return launch(h, a, (hipStream_t)stream);
+}
+
+int mapfx_step(mapfx_t* h, const mapfx_state* st, const void* actions, int action_dtype,
+               const mapfx_out* out, void* stream) {
+  if (!h) return set_error(MAPFX_EINVAL, "NULL handle");
+  int rc = check_state(h, st, false);
+  if (rc) return rc;
+  if ((rc = check_out(h, out))) return rc;
+  if (!actions) return set_error(MAPFX_EINVAL, "NULL actions");
+  if (action_dtype < MAPFX_I8 || action_dtype > MAPFX_I64)
+    return set_error(MAPFX_EINVAL, "bad action_dtype %d", action_dtype);
+  Args a;
+  memset(&a, 0, sizeof(a));
+  fill_state_args(a, st);
+  fill_out_args(a, out);
+  a.actions = actions;
+  a.act_dtype = action_dtype;
+  a.T = 1;
+  a.do_step = 1;
+  a.pow_lut = h->pow_lut;
+  return launch(h, a, (hipStream_t)stream);
+}
+
+int mapfx_rollout(mapfx_t* h, const mapfx_state* st, int32_t T, const void* actions,
+                  int action_dtype, uint64_t seed, int32_t t0, int32_t autoreset,
+                  const mapfx_out* traj, void* stream) {
+  if (!h) return set_error(MAPFX_EINVAL, "NULL handle");
+  int rc = check_state(h, st, autoreset != 0);
+  if (rc) return rc;
+  if ((rc = check_out(h, traj))) return rc;
+  if (T < 0) return set_error(MAPFX_EINVAL, "T < 0");
+  if (T == 0) return MAPFX_OK;
+  if (actions && (action_dtype < MAPFX_I8 || action_dtype > MAPFX_I64))
+    return set_error(MAPFX_EINVAL, "bad action_dtype %d", action_dtype);
+  Args a;
+  memset(&a, 0, sizeof(a));
+  fill_state_args(a, st);
+  fill_out_args(a, traj);
+  a.actions = actions;
+  a.act_dtype = action_dtype;
+  a.use_rng = actions ? 0 : 1;
+  a.seed = seed;
+  a.t0 = t0;
+  a.T = T;
+  a.autoreset = autoreset ? 1 : 0;
+  a.do_step = 1;
+  a.pow_lut = h->pow_lut;
+  return launch(h, a, (hipStream_t)stream);
+}
+
+int mapfx_gen_actions(mapfx_t* h, uint64_t seed, int32_t t0, int32_t T, int8_t* out,
+                      void* stream) {
+  if (!h || !out) return set_error(MAPFX_EINVAL, "NULL handle/out");
+  if (T < 0) return set_error(MAPFX_EINVAL, "T < 0");
+  const long long total = (long long)T * h->geo.E * h->geo.N;
+  if (total == 0) return MAPFX_OK;
+  const int bt = 256;
+  hipLaunchKernelGGL(gen_actions_kernel, dim3((unsigned)((total + bt - 1) / bt)), dim3(bt), 0,
+                     (hipStream_t)stream, total, h->geo.E, h->geo.N, (long long)h->geo.env_offset,
+                     seed, t0, out);
+  return check_hip(hipGetLastError(), "gen_actions_kernel launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,105 @@
+"""ctypes binding of the C ABI declared in include/mapfx.h (libmapfx.so).
+
+torch is imported first so that the HIP runtime torch already loaded
+(libamdhip64.so.7) is the one libmapfx.so binds to: device pointers and
+streams then come straight from torch tensors / torch.cuda streams.
+
+There is no fallback: if the library is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede loading libmapfx.so: shared HIP runtime)
+
+LIB_NAME = "libmapfx.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+MAPFX_OBS_FULL = 1
+MAPFX_OBS_WINDOW = 2
+MAPFX_OBS_PRIMAL = 4
+MAPFX_I8, MAPFX_I32, MAPFX_I64 = 0, 1, 2
+
+c_i32, c_i64, c_u64, c_f64, c_vp = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64,
+                                    ctypes.c_double, ctypes.c_void_p)
+
+
+class Cfg(ctypes.Structure):
+    _fields_ = [("H", c_i32), ("W", c_i32), ("n_agents", c_i32), ("n_envs", c_i32),
+                ("env_offset", c_i64), ("episode_limit", c_i32), ("step_reward", c_f64),
+                ("collide_reward", c_f64), ("obs_mode", c_i32), ("window", c_i32),
+                ("primal_size", c_i32), ("map_shared", c_i32)]
+
+
+class State(ctypes.Structure):
+    _fields_ = [("pos", c_vp), ("goal", c_vp), ("init_pos", c_vp), ("done", c_vp), ("t", c_vp),
+                ("steps", c_vp), ("map_bits", c_vp)]
+
+
+class Out(ctypes.Structure):
+    _fields_ = [("reward", c_vp), ("reward_f32", c_vp), ("term", c_vp), ("node", c_vp),
+                ("edge", c_vp), ("avail", c_vp), ("obs_full", c_vp), ("obs_window", c_vp),
+                ("obs_primal", c_vp), ("primal_vec", c_vp), ("traj_pos", c_vp),
+                ("traj_done", c_vp), ("traj_t", c_vp), ("err", c_vp)]
+
+
+class Info(ctypes.Structure):
+    _fields_ = [("lanes_per_env", c_i32), ("agents_per_lane", c_i32), ("envs_per_block", c_i32),
+                ("block_threads", c_i32), ("lds_bytes", c_i32), ("cell_bytes", c_i32),
+                ("pad", c_i32)]
+
+
+# every symbol include/mapfx.h declares (checked by tests/test_abi_exports.py)
+EXPORTS = ("mapfx_abi_version", "mapfx_last_error", "mapfx_map_stride", "mapfx_obs_elem_size",
+           "mapfx_create", "mapfx_destroy", "mapfx_query", "mapfx_reset", "mapfx_step",
+           "mapfx_observe", "mapfx_rollout", "mapfx_gen_actions", "mapfx_action")
+
+
+class MapfxError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("%s not built: run `python -c 'import __graft_entry__ as g; g.build()'`"
+                          % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    sig = {
+        "mapfx_abi_version": (c_i32, []),
+        "mapfx_last_error": (ctypes.c_char_p, []),
+        "mapfx_map_stride": (c_i64, [c_i32, c_i32]),
+        "mapfx_obs_elem_size": (c_i32, [c_i32]),
+        "mapfx_create": (c_i32, [P(Cfg), P(c_vp)]),
+        "mapfx_destroy": (None, [c_vp]),
+        "mapfx_query": (c_i32, [c_vp, P(Info)]),
+        "mapfx_reset": (c_i32, [c_vp, P(State), c_vp, P(Out), c_vp]),
+        "mapfx_step": (c_i32, [c_vp, P(State), c_vp, c_i32, P(Out), c_vp]),
+        "mapfx_observe": (c_i32, [c_vp, P(State), P(Out), c_vp]),
+        "mapfx_rollout": (c_i32, [c_vp, P(State), c_i32, c_vp, c_i32, c_u64, c_i32, c_i32, P(Out),
+                                  c_vp]),
+        "mapfx_gen_actions": (c_i32, [c_vp, c_u64, c_i32, c_i32, c_vp, c_vp]),
+        "mapfx_action": (c_i32, [c_u64, c_i64, c_i32, c_i32]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib.mapfx_last_error()
+        raise MapfxError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()

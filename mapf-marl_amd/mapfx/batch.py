@@ -1,0 +1,242 @@
+"""MapfGridBatch — E device-resident MAPF_GRID envs stepped by one HIP launch.
+
+The batched counterpart of the reference's env + ParallelRunner pair
+(MARL-curve-main/src/envs/mapf_gridworld.py, runners/parallel_runner.py:91-206):
+state, actions and every output stay in HBM as torch tensors; the C ABI
+(include/mapfx.h, via mapfx._abi) is called with their device pointers on the
+current torch stream.  Nothing here computes env semantics on the host.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _abi
+from ._abi import MAPFX_I8, MAPFX_I32, MAPFX_I64, MAPFX_OBS_FULL, MAPFX_OBS_PRIMAL, \
+    MAPFX_OBS_WINDOW, check, lib, ptr
+from .maps import map_stride, pack_bits
+
+_DTYPES = {torch.int8: MAPFX_I8, torch.int32: MAPFX_I32, torch.int64: MAPFX_I64}
+OBS_MODES = {"full": MAPFX_OBS_FULL, "window": MAPFX_OBS_WINDOW, "primal": MAPFX_OBS_PRIMAL}
+
+
+def _stream_handle() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+class MapfGridBatch:
+    """E independent MAPF_GRID envs on one GPU.
+
+    Parameters mirror MAPF_GRID.__init__ (envs/mapf_gridworld.py:21-32) plus the
+    batch description: `grids` is [E|1, H, W] (nonzero = obstacle) or
+    precomputed `bits` [E|1, map_stride]; `init_pos` / `goals` are [E, N, 2]
+    (row, col).  `obs` selects which observation kinds are produced each step:
+    "full" (get_obs/get_state occupancy), "window" (marl_partial window of
+    `window`), "primal" (PRIMAL _observe of `primal_size`).
+    """
+
+    def __init__(self, init_pos, goals, grids=None, bits=None, hw=None, episode_limit=10000,
+                 step_reward=-0.01, collide_reward=-10, obs=("full",), window=5,
+                 primal_size=10, device=None, env_offset=0, track_steps=True):
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise RuntimeError("MapfGridBatch runs on a HIP device only (got %s)" % self.device)
+        init_pos = torch.as_tensor(np.asarray(init_pos), dtype=torch.int32)
+        goals = torch.as_tensor(np.asarray(goals), dtype=torch.int32)
+        if init_pos.ndim != 3 or init_pos.shape[-1] != 2 or goals.shape != init_pos.shape:
+            raise ValueError("init_pos/goals must both be [E, N, 2]")
+        self.E, self.N = int(init_pos.shape[0]), int(init_pos.shape[1])
+        if bits is None:
+            g = np.asarray(grids)
+            if g.ndim == 2:
+                g = g[None]
+            self.H, self.W = int(g.shape[1]), int(g.shape[2])
+            bits = pack_bits(g)
+        else:
+            self.H, self.W = hw
+        bits = np.asarray(bits, dtype=np.uint8)
+        if bits.ndim == 1:
+            bits = bits[None]
+        if bits.shape[1] != map_stride(self.H, self.W) or bits.shape[0] not in (1, self.E):
+            raise ValueError("bits must be [E or 1, %d]" % map_stride(self.H, self.W))
+        ip, gl = init_pos.numpy(), goals.numpy()
+        for name, arr in (("init_pos", ip), ("goals", gl)):
+            if arr.size and (arr[..., 0].min() < 0 or arr[..., 0].max() >= self.H
+                             or arr[..., 1].min() < 0 or arr[..., 1].max() >= self.W):
+                raise ValueError("%s outside the %dx%d grid" % (name, self.H, self.W))
+        self.map_shared = bits.shape[0] == 1 and self.E != 1
+        self.episode_limit = int(episode_limit)
+        self.step_reward = step_reward
+        self.collide_reward = collide_reward
+        self.obs_kinds = tuple(obs)
+        mode = 0
+        for k in self.obs_kinds:
+            mode |= OBS_MODES[k]
+        self.window, self.primal_size = int(window), int(primal_size)
+
+        cfg = _abi.Cfg(H=self.H, W=self.W, n_agents=self.N, n_envs=self.E,
+                       env_offset=int(env_offset), episode_limit=self.episode_limit,
+                       step_reward=float(step_reward), collide_reward=float(collide_reward),
+                       obs_mode=mode, window=self.window, primal_size=self.primal_size,
+                       map_shared=1 if self.map_shared else 0)
+        self._cfg = cfg
+        with torch.cuda.device(self.device):
+            h = ctypes.c_void_p()
+            check(lib.mapfx_create(ctypes.byref(cfg), ctypes.byref(h)), "mapfx_create")
+        self._h = h
+        dev = self.device
+        self.bits = torch.as_tensor(bits).to(dev)
+        self.init_pos = init_pos.to(dev).contiguous()
+        self.goal = goals.to(dev).contiguous()
+        self.pos = self.init_pos.clone()
+        self.done = torch.zeros((self.E, self.N), dtype=torch.uint8, device=dev)
+        self.t = torch.zeros((self.E,), dtype=torch.int32, device=dev)
+        self.steps = torch.zeros((self.E, self.N), dtype=torch.int32, device=dev) \
+            if track_steps else None
+        self.err = torch.zeros((1,), dtype=torch.int32, device=dev)
+        self.obs_elem = torch.int8 if lib.mapfx_obs_elem_size(self.N) == 1 else torch.int16
+        self.out = self._alloc_out(None)
+        self._state = _abi.State(pos=ptr(self.pos), goal=ptr(self.goal),
+                                 init_pos=ptr(self.init_pos), done=ptr(self.done), t=ptr(self.t),
+                                 steps=ptr(self.steps), map_bits=ptr(self.bits))
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc_out(self, T):
+        E, N, dev = self.E, self.N, self.device
+        lead = () if T is None else (T,)
+        o = {
+            "reward": torch.zeros(lead + (E,), dtype=torch.float64, device=dev),
+            "reward_f32": torch.zeros(lead + (E,), dtype=torch.float32, device=dev),
+            "term": torch.zeros(lead + (E,), dtype=torch.uint8, device=dev),
+            "node": torch.zeros(lead + (E, N), dtype=torch.uint8, device=dev),
+            "edge": torch.zeros(lead + (E, N), dtype=torch.uint8, device=dev),
+            "avail": torch.zeros(lead + (E, N), dtype=torch.uint8, device=dev),
+        }
+        if "full" in self.obs_kinds:
+            o["obs_full"] = torch.zeros(lead + (E, self.H * self.W), dtype=self.obs_elem,
+                                        device=dev)
+        if "window" in self.obs_kinds:
+            w = self.window
+            o["obs_window"] = torch.zeros(lead + (E, N, 2, w, w), dtype=self.obs_elem, device=dev)
+        if "primal" in self.obs_kinds:
+            s = self.primal_size
+            o["obs_primal"] = torch.zeros(lead + (E, N, 4, s, s), dtype=torch.uint8, device=dev)
+            o["primal_vec"] = torch.zeros(lead + (E, N, 3), dtype=torch.float64, device=dev)
+        if T is not None:
+            o["traj_pos"] = torch.zeros((T, E, N, 2), dtype=torch.int32, device=dev)
+            o["traj_done"] = torch.zeros((T, E, N), dtype=torch.uint8, device=dev)
+            o["traj_t"] = torch.zeros((T, E), dtype=torch.int32, device=dev)
+        return o
+
+    def _out_struct(self, o, keys=None):
+        s = _abi.Out()
+        for name, _ in _abi.Out._fields_:
+            if name == "err":
+                continue
+            if keys is not None and name not in keys:
+                continue
+            if name in o:
+                setattr(s, name, ptr(o[name]))
+        s.err = ptr(self.err)
+        return s
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.mapfx_destroy(h)
+            self._h = None
+
+    def info(self):
+        inf = _abi.Info()
+        check(lib.mapfx_query(self._h, ctypes.byref(inf)), "mapfx_query")
+        return {k: getattr(inf, k) for k, _ in _abi.Info._fields_}
+
+    # ------------------------------------------------------------------ API
+    def reset(self, env_mask=None):
+        """envs/mapf_gridworld.py:70-83 for the masked envs (all if None);
+        refreshes obs/avail/term of every env.  Returns self.out."""
+        m = None
+        if env_mask is not None:
+            m = torch.as_tensor(env_mask, device=self.device).to(torch.uint8).contiguous()
+        o = self._out_struct(self.out, keys=("term", "avail", "obs_full", "obs_window",
+                                             "obs_primal", "primal_vec"))
+        with torch.cuda.device(self.device):
+            check(lib.mapfx_reset(self._h, ctypes.byref(self._state), ptr(m), ctypes.byref(o),
+                                  _stream_handle()), "mapfx_reset")
+        return self.out
+
+    def observe(self):
+        o = self._out_struct(self.out, keys=("term", "avail", "obs_full", "obs_window",
+                                             "obs_primal", "primal_vec"))
+        with torch.cuda.device(self.device):
+            check(lib.mapfx_observe(self._h, ctypes.byref(self._state), ctypes.byref(o),
+                                    _stream_handle()), "mapfx_observe")
+        return self.out
+
+    def step(self, actions, outputs=None):
+        """One env step of all E envs.  actions: [E, N] int8/int32/int64 tensor.
+        `outputs` optionally restricts which outputs are written (names of self.out)."""
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype not in _DTYPES:
+            a = a.to(torch.int64)
+        a = a.contiguous()
+        if tuple(a.shape) != (self.E, self.N):
+            raise AssertionError("actions must be [%d, %d], got %s" % (self.E, self.N,
+                                                                     tuple(a.shape)))
+        o = self._out_struct(self.out, keys=outputs)
+        with torch.cuda.device(self.device):
+            check(lib.mapfx_step(self._h, ctypes.byref(self._state), ptr(a), _DTYPES[a.dtype],
+                                 ctypes.byref(o), _stream_handle()), "mapfx_step")
+        return self.out
+
+    def rollout(self, T, actions=None, seed=0, t0=0, autoreset=False, traj=None, outputs=None):
+        """T fused steps in one launch.  actions: [T, E, N] tensor or None (device
+        generator keyed by (seed, global env, t0+k, agent)).  Returns the
+        trajectory dict ([T, ...] tensors), allocated unless `traj` is given."""
+        if traj is None:
+            traj = self._alloc_out(T)
+        ap, adt = None, MAPFX_I8
+        if actions is not None:
+            actions = torch.as_tensor(actions, device=self.device)
+            if actions.dtype not in _DTYPES:
+                actions = actions.to(torch.int64)
+            actions = actions.contiguous()
+            if tuple(actions.shape) != (T, self.E, self.N):
+                raise AssertionError("actions must be [T, E, N]")
+            ap, adt = ptr(actions), _DTYPES[actions.dtype]
+        o = self._out_struct(traj, keys=outputs)
+        with torch.cuda.device(self.device):
+            check(lib.mapfx_rollout(self._h, ctypes.byref(self._state), int(T), ap, adt,
+                                    int(seed) & 0xFFFFFFFFFFFFFFFF, int(t0), 1 if autoreset else 0,
+                                    ctypes.byref(o), _stream_handle()), "mapfx_rollout")
+        return traj
+
+    def gen_actions(self, T, seed, t0=0, out=None):
+        if out is None:
+            out = torch.empty((T, self.E, self.N), dtype=torch.int8, device=self.device)
+        with torch.cuda.device(self.device):
+            check(lib.mapfx_gen_actions(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(t0), int(T),
+                                        ptr(out), _stream_handle()), "mapfx_gen_actions")
+        return out
+
+    def check_err(self):
+        """Raise AssertionError like the reference (:91-92) if an env got an
+        action outside 0..4 since the last call (synchronises)."""
+        e = int(self.err.item())
+        if e:
+            self.err.zero_()
+            raise AssertionError("invalid action for env %d (actions must be in 0..4)" % (e - 1))
+
+    # --------------------------------------------------- PyMARL-shaped views
+    def avail_actions(self, avail=None):
+        """[E, N, 5] int64 0/1, the layout of get_avail_actions (:198-224)."""
+        m = self.out["avail"] if avail is None else avail
+        bits = torch.arange(5, device=m.device, dtype=torch.uint8)
+        return ((m.unsqueeze(-1) >> bits) & 1).to(torch.int64)
+
+    def full_obs(self):
+        """[E, N, H*W] view: every agent observes the same occupancy map (:161-183)."""
+        o = self.out["obs_full"]
+        return o.unsqueeze(1).expand(self.E, self.N, o.shape[-1])

@@ -1,0 +1,335 @@
+"""GPU parity: the HIP path (through the C ABI) vs the reference golden vectors
+and vs the C oracle on seeded batched inputs.  Bit-exact for every output:
+positions, dones, node/edge collisions, fp64 rewards (bit patterns), avail
+masks, occupancy / window / PRIMAL observations."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import fixture_rewards, load_fixture, primal_fixtures, step_fixtures
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mapfx_mod():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mapfx
+    return mapfx
+
+
+def _u64(x):
+    return np.ascontiguousarray(x).view(np.uint64)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+# ---------------------------------------------------------------------------
+# 1. golden vectors from the reference (single env)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", step_fixtures())
+def test_step_matches_reference_goldens(mapfx_mod, name):
+    fx = load_fixture(name)
+    sr, cr = fixture_rewards(fx)
+    windows = sorted(int(k[6:]) for k in fx if k.startswith("window") and k != "window_steps")
+    wsteps = list(fx["window_steps"])
+    h, w = fx["grid"].shape
+    for win in windows:
+        b = mapfx_mod.MapfGridBatch(fx["init_pos"][None], fx["goals"][None],
+                                    grids=fx["grid"][None], episode_limit=int(fx["meta_limit"]),
+                                    step_reward=sr, collide_reward=cr, obs=("full", "window"),
+                                    window=win)
+        out = b.reset()
+        assert np.array_equal(_np(out["obs_full"][0]).reshape(h, w), fx["occ0"])
+        mask0 = (fx["avail0"].astype(np.uint8) << np.arange(5, dtype=np.uint8)).sum(-1)
+        assert np.array_equal(_np(out["avail"][0]), mask0)
+        acts = torch.from_numpy(fx["actions"].astype(np.int64)).cuda()  # PyMARL hands int64
+        for t in range(fx["actions"].shape[0]):
+            out = b.step(acts[t][None])
+            assert _u64(_np(out["reward"]))[0] == _u64(fx["reward"][t:t + 1])[0], (t, win)
+            assert np.array_equal(_np(b.pos[0]), fx["pos"][t]), t
+            assert np.array_equal(_np(b.done[0]), fx["done"][t]), t
+            assert np.array_equal(_np(out["node"][0]), fx["node"][t]), t
+            assert np.array_equal(_np(out["edge"][0]), fx["edge"][t]), t
+            assert np.array_equal(_np(b.avail_actions()[0]), fx["avail"][t].astype(np.int64)), t
+            assert int(_np(b.t)[0]) == int(fx["t"][t])
+            assert bool(_np(out["term"])[0]) == bool(fx["done"][t].all())
+            if "occ" in fx:
+                assert np.array_equal(_np(out["obs_full"][0]).reshape(h, w), fx["occ"][t]), t
+            if t in wsteps:
+                wi = wsteps.index(t)
+                assert np.array_equal(_np(out["obs_window"][0]), fx["window%d" % win][wi]), \
+                    (t, win)
+        assert int(b.err.item()) == 0
+
+
+@pytest.mark.parametrize("name", primal_fixtures())
+def test_primal_matches_reference_goldens(mapfx_mod, name):
+    fx = load_fixture(name)
+    E = fx["pos"].shape[0]
+    goals = np.broadcast_to(fx["goals"][None], (E,) + fx["goals"].shape)
+    for s in [int(v) for v in np.atleast_1d(fx["meta_sizes"])]:
+        b = mapfx_mod.MapfGridBatch(fx["pos"], goals, grids=fx["grid"][None].repeat(E, 0),
+                                    obs=("primal",), primal_size=s)
+        out = b.reset()
+        assert np.array_equal(_np(out["obs_primal"]), fx["maps%d" % s]), s
+        assert np.array_equal(_u64(_np(out["primal_vec"])), _u64(fx["vec%d" % s])), s
+
+
+# ---------------------------------------------------------------------------
+# 2. batched parity vs the C oracle (configs of BASELINE.json + odd shapes)
+# ---------------------------------------------------------------------------
+CONFIGS = [
+    # name, E, H(=W), N, p_obst, steps, window, shared_warehouse, limit
+    ("c1_8x8_n2", 64, 8, 2, 0.0, 60, 5, False, 2000),
+    ("c2_32x32_n16", 4096, 32, 16, 0.10, 24, 5, False, 2000),
+    ("c3_wh64_n64", 512, 64, 64, None, 12, 5, True, 2000),
+    ("c5_128_n256", 32, 128, 256, 0.10, 6, 5, False, 2000),
+    ("odd_13x13_n5_w7", 300, 13, 5, 0.25, 40, 7, False, 17),
+    ("dense_10x10_n90", 40, 10, 90, 0.05, 30, 3, False, 2000),
+    ("n200_24x24", 12, 24, 200, 0.05, 10, 5, False, 2000),
+    ("n300_40x40_apl2", 6, 40, 300, 0.05, 8, 4, False, 2000),
+]
+
+
+def _instances(mapfx_mod, E, S, N, p, shared, seed=3):
+    from mapfx.maps import synthetic_instances, warehouse_grid
+    if shared:
+        return synthetic_instances(E, S, S, N, seed=seed, shared_grid=warehouse_grid(S))
+    return synthetic_instances(E, S, S, N, p_obstacle=p, seed=seed)
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=[c[0] for c in CONFIGS])
+def test_batched_step_matches_oracle(mapfx_mod, cfg):
+    from oracle import corc
+    name, E, S, N, p, T, win, shared, limit = cfg
+    inst = _instances(mapfx_mod, E, S, N, p, shared)
+    init = inst["init_pos"].copy()
+    if name.startswith("dense"):   # stacked starts / starts on obstacles (quirks 1, 3)
+        rs = np.random.RandomState(1)
+        init = rs.randint(0, S, size=(E, N, 2)).astype(np.int32)
+    b = mapfx_mod.MapfGridBatch(init, inst["goals"], bits=inst["bits"], hw=(S, S),
+                                episode_limit=limit, obs=("full", "window"), window=win)
+    ob = corc.OracleBatch(inst["bits"], init, inst["goals"], S, S, limit=limit)
+    out = b.reset()
+    ref = ob.observe(window=win)
+    assert np.array_equal(_np(out["obs_full"]), ref["obs_full"])
+    assert np.array_equal(_np(out["obs_window"]), ref["obs_window"])
+    rs = np.random.RandomState(7)
+    for t in range(T):
+        a = rs.randint(0, 5, size=(E, N)).astype(np.int8)
+        out = b.step(torch.from_numpy(a).cuda())
+        rstep = ob.step(a.astype(np.int32))
+        ref = ob.observe(window=win)
+        assert np.array_equal(_np(b.pos), ob.pos), (name, t)
+        assert np.array_equal(_np(b.done), ob.done), (name, t)
+        assert np.array_equal(_np(b.t), ob.t), (name, t)
+        assert np.array_equal(_np(b.steps), ob.steps), (name, t)
+        assert np.array_equal(_u64(_np(out["reward"])), _u64(rstep["reward"])), (name, t)
+        assert np.array_equal(_np(out["reward_f32"]), rstep["reward"].astype(np.float32))
+        assert np.array_equal(_np(out["node"]), rstep["node"]), (name, t)
+        assert np.array_equal(_np(out["edge"]), rstep["edge"]), (name, t)
+        assert np.array_equal(_np(out["avail"]), ref["avail"]), (name, t)
+        assert np.array_equal(_np(out["term"]), ref["term"]), (name, t)
+        assert np.array_equal(_np(out["obs_full"]), ref["obs_full"]), (name, t)
+        assert np.array_equal(_np(out["obs_window"]), ref["obs_window"]), (name, t)
+
+
+@pytest.mark.parametrize("S,N,s,E", [(32, 16, 10, 64), (64, 32, 10, 16), (20, 30, 7, 50),
+                                     (128, 200, 11, 4)])
+def test_batched_primal_matches_oracle(mapfx_mod, S, N, s, E):
+    from mapfx.maps import synthetic_instances
+    from oracle import corc
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.15, seed=4)
+    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                                obs=("primal", "window"), primal_size=s, window=5)
+    ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S)
+    rs = np.random.RandomState(2)
+    b.reset()
+    for t in range(6):
+        a = rs.randint(0, 5, size=(E, N)).astype(np.int8)
+        out = b.step(torch.from_numpy(a).cuda())
+        ob.step(a.astype(np.int32))
+        ref = ob.observe(psize=s, full=False, win=True, primal=True)
+        assert np.array_equal(_np(out["obs_primal"]), ref["obs_primal"]), t
+        assert np.array_equal(_u64(_np(out["primal_vec"])), _u64(ref["primal_vec"])), t
+        assert np.array_equal(_np(out["obs_window"]), ref["obs_window"]), t
+
+
+# ---------------------------------------------------------------------------
+# 3. fused rollout == repeated steps; device generator == host generator
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("S,N,E,T", [(32, 16, 1000, 20), (8, 2, 300, 50), (64, 64, 40, 8),
+                                     (128, 256, 4, 4)])
+def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T):
+    from mapfx import rng
+    from mapfx.maps import synthetic_instances
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=5)
+    kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=35, obs=("full", "window", "primal"),
+              window=5, primal_size=10)
+    b1 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], env_offset=1000, **kw)
+    b2 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], env_offset=1000, **kw)
+    b1.reset()
+    b2.reset()
+    seed, t0 = 99, 3
+    acts = b2.gen_actions(T, seed, t0=t0)
+    host = rng.gen_actions(seed, np.arange(1000, 1000 + E), np.arange(t0, t0 + T), N)
+    assert np.array_equal(_np(acts), host)
+    traj = b1.rollout(T, seed=seed, t0=t0)
+    traj_buf = b2.rollout(T, actions=acts.to(torch.int32))  # actions read from HBM
+    b3 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], env_offset=1000, **kw)
+    b3.reset()
+    for k in range(T):
+        out = b3.step(acts[k])
+        for key in ("reward", "node", "edge", "avail", "term", "obs_full", "obs_window",
+                    "obs_primal", "primal_vec"):
+            x = _np(out[key])
+            for tr in (traj, traj_buf):
+                y = _np(tr[key][k])
+                if x.dtype == np.float64:
+                    assert np.array_equal(_u64(x), _u64(y)), (key, k)
+                else:
+                    assert np.array_equal(x, y), (key, k)
+        for tr in (traj, traj_buf):
+            assert np.array_equal(_np(tr["traj_pos"][k]), _np(b3.pos)), k
+            assert np.array_equal(_np(tr["traj_done"][k]), _np(b3.done)), k
+            assert np.array_equal(_np(tr["traj_t"][k]), _np(b3.t)), k
+    for bb in (b1, b2):
+        assert np.array_equal(_np(bb.pos), _np(b3.pos))
+        assert np.array_equal(_np(bb.done), _np(b3.done))
+        assert np.array_equal(_np(bb.t), _np(b3.t))
+        assert np.array_equal(_np(bb.steps), _np(b3.steps))
+
+
+def test_rollout_matches_oracle_long_horizon(mapfx_mod):
+    """C2 shape (32x32, 16 agents, 4096 envs), 64 fused steps vs the C oracle."""
+    from mapfx.maps import synthetic_instances
+    from oracle import corc
+    E, S, N, T = 4096, 32, 16, 64
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=1)
+    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                                episode_limit=2000, obs=("window",))
+    ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=2000)
+    b.reset()
+    traj = b.rollout(T, seed=2, t0=0)
+    ref = ob.rollout(T, seed=2, t0=0)
+    assert np.array_equal(_np(b.pos), ob.pos)
+    assert np.array_equal(_np(b.done), ob.done)
+    assert np.array_equal(_np(b.t), ob.t)
+    assert np.array_equal(_u64(_np(traj["reward"][-1])), _u64(ref["reward"]))
+    assert np.array_equal(_np(traj["node"][-1]), ref["node"])
+    assert np.array_equal(_np(traj["edge"][-1]), ref["edge"])
+    assert np.array_equal(_np(traj["avail"][-1]), ref["avail"])
+    assert np.array_equal(_np(traj["obs_window"][-1]), ref["obs_window"])
+
+
+def test_autoreset(mapfx_mod):
+    """Envs whose agents are all done restart from init_pos in the fused rollout,
+    identically to step + reset(mask)."""
+    from mapfx.maps import synthetic_instances
+    E, S, N, T, limit = 64, 8, 3, 30, 7
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=6)
+    kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=limit, obs=("window",))
+    b1 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
+    b2 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
+    b1.reset()
+    b2.reset()
+    acts = b2.gen_actions(T, 5)
+    traj = b1.rollout(T, actions=acts, autoreset=True)
+    resets = 0
+    for k in range(T):
+        out = b2.step(acts[k])
+        assert np.array_equal(_u64(_np(out["reward"])), _u64(_np(traj["reward"][k]))), k
+        assert np.array_equal(_np(out["obs_window"]), _np(traj["obs_window"][k])), k
+        assert np.array_equal(_np(b2.pos), _np(traj["traj_pos"][k])), k
+        term = out["term"].clone()
+        resets += int(term.sum())
+        if term.any():
+            b2.reset(env_mask=term)
+    assert resets >= E  # limit 7 over 30 steps: every env resets several times
+    assert np.array_equal(_np(b1.pos), _np(b2.pos))
+    assert np.array_equal(_np(b1.t), _np(b2.t))
+    assert np.array_equal(_np(b1.done), _np(b2.done))
+
+
+def test_invalid_action_sets_err_and_skips_env(mapfx_mod):
+    from mapfx.maps import synthetic_instances
+    E, S, N = 8, 8, 4
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=8)
+    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S))
+    b.reset()
+    a = torch.full((E, N), 1, dtype=torch.int64, device="cuda")
+    a[3, 2] = 7
+    pos0 = _np(b.pos).copy()
+    b.step(a)
+    assert np.array_equal(_np(b.pos)[3], pos0[3]) and int(_np(b.t)[3]) == 0
+    assert int(_np(b.t)[0]) == 1
+    with pytest.raises(AssertionError):
+        b.check_err()
+    b.step(torch.full((E, N), 4, dtype=torch.int64, device="cuda"))
+    b.check_err()
+
+
+# ---------------------------------------------------------------------------
+# 4. the MAPF_GRID drop-in class (plugin surface) on the golden vectors
+# ---------------------------------------------------------------------------
+def _write_map_and_scen(tmp_path, grid, n):
+    s = grid.shape[0]
+    mp = tmp_path / "g.map"
+    rows = ["".join("." if v == 0 else "@" for v in row) for row in grid]
+    mp.write_text("type octile\nheight %d\nwidth %d\nmap\n" % (s, s) + "\n".join(rows) + "\n")
+    prefix = str(tmp_path / "g-random-")
+    for k in range(1, 26):
+        with open(prefix + "%d.scen" % k, "w") as f:
+            f.write("version 1\n")
+            for i in range(max(n, 30)):
+                f.write("0\tg.map\t%d\t%d\t%d\t%d\t%d\t%d\t0\n" % (s, s, i % s, (i // s) % s,
+                                                                 (i * 7) % s, (i * 3) % s))
+    return str(mp), prefix
+
+
+@pytest.mark.parametrize("name", ["c1_empty8_n2", "edge6_scripted", "empty8_int_rewards",
+                                  "dense8_n30", "edge6_float_collide"])
+def test_dropin_mapf_grid_on_goldens(mapfx_mod, tmp_path, name):
+    from mapfx.envs import REGISTRY
+    fx = load_fixture(name)
+    sr, cr = fixture_rewards(fx)
+    n = fx["init_pos"].shape[0]
+    mp, prefix = _write_map_and_scen(tmp_path, fx["grid"], n)
+    env = REGISTRY["mapf_gridworld"](grid_file_path=mp, agents_path=prefix, n_agents=n,
+                                     episode_limit=int(fx["meta_limit"]), step_reward=sr,
+                                     collide_reward=cr)
+    for a in range(n):   # inject the fixture's scenario, as gen_fixtures.py did
+        env._agent_init_pos[a] = tuple(int(v) for v in fx["init_pos"][a])
+        env._agent_goal_pos[a] = tuple(int(v) for v in fx["goals"][a])
+    env.agent_starts = [env._agent_init_pos[i] for i in range(n)]
+    env.agent_goals = [env._agent_goal_pos[i] for i in range(n)]
+    obs = env.reset()
+    assert obs.shape == (n, fx["occ0"].size) and obs.dtype == np.int64
+    assert np.array_equal(obs[0], fx["occ0"].reshape(-1))
+    assert env.get_avail_actions() == fx["avail0"].astype(int).tolist()
+    info = env.get_env_info()
+    assert info["n_actions"] == 5 and info["state_shape"] == fx["occ0"].size
+    dones_ref = None
+    for t in range(fx["actions"].shape[0]):
+        R, dones, inf = env.step(fx["actions"][t].astype(np.int64))
+        if dones_ref is None:
+            dones_ref = dones
+        assert dones is dones_ref is env._agent_dones   # aliased list (quirk 6)
+        assert isinstance(R, int) == bool(fx["reward_is_int"][t])
+        assert np.float64(R).view(np.uint64) == fx["reward"][t:t + 1].view(np.uint64)[0]
+        assert [int(v) for v in dones] == fx["done"][t].tolist()
+        assert env.agent_positions == [tuple(p) for p in fx["pos"][t].tolist()]
+        assert env.get_avail_actions() == fx["avail"][t].astype(int).tolist()
+        assert inf == {"_step_count": int(fx["t"][t])}
+        if "occ" in fx:
+            assert np.array_equal(env.get_state(), fx["occ"][t].reshape(-1))
+            assert np.array_equal(env.get_obs()[n - 1], fx["occ"][t].reshape(-1))
+        assert env.episode_done() == bool(fx["done"][t].all())
+    with pytest.raises(AssertionError):
+        env.step([0] * (n + 1))
+    with pytest.raises(AssertionError):
+        env.step([5] + [0] * (n - 1))

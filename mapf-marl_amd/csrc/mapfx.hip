@@ -820,7 +820,9 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
       delete h;
       return set_error(MAPFX_ENOMEM, "host LUT allocation failed");
     }
-    for (int i = 0; i < n; ++i) lut[i] = pow((double)i, 0.5);
+    // through a volatile pointer: clang would otherwise rewrite pow(x, 0.5) as sqrt(x)
+    double (*volatile libm_pow)(double, double) = pow;
+    for (int i = 0; i < n; ++i) lut[i] = libm_pow((double)i, 0.5);
     hipError_t e = hipMalloc((void**)&h->pow_lut, sizeof(double) * n);
     if (e == hipSuccess) e = hipMemcpy(h->pow_lut, lut, sizeof(double) * n, hipMemcpyHostToDevice);
     free(lut);

@@ -43,8 +43,8 @@ class MapfGridBatch:
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("MapfGridBatch runs on a HIP device only (got %s)" % self.device)
-        init_pos = torch.as_tensor(np.asarray(init_pos), dtype=torch.int32)
-        goals = torch.as_tensor(np.asarray(goals), dtype=torch.int32)
+        init_pos = torch.as_tensor(np.array(init_pos, dtype=np.int32))
+        goals = torch.as_tensor(np.array(goals, dtype=np.int32))
         if init_pos.ndim != 3 or init_pos.shape[-1] != 2 or goals.shape != init_pos.shape:
             raise ValueError("init_pos/goals must both be [E, N, 2]")
         self.E, self.N = int(init_pos.shape[0]), int(init_pos.shape[1])
@@ -56,7 +56,7 @@ class MapfGridBatch:
             bits = pack_bits(g)
         else:
             self.H, self.W = hw
-        bits = np.asarray(bits, dtype=np.uint8)
+        bits = np.array(bits, dtype=np.uint8)
         if bits.ndim == 1:
             bits = bits[None]
         if bits.shape[1] != map_stride(self.H, self.W) or bits.shape[0] not in (1, self.E):

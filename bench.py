@@ -1,0 +1,302 @@
+#!/usr/bin/env python3
+"""Benchmark of the batched MAPF gridworld step (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 32x32 grids with
+i.i.d. 10% obstacles per env, 16 agents, 4096 envs per GPU (weak scaling:
+every rank owns 4096 envs with globally keyed seeds), marl_partial 5x5 window
+observations, uniform random actions resident in HBM.
+
+A "step" is one env step of every env of the batch: actions read from HBM,
+moves + vertex/edge collisions + fp64 rewards + dones, and every per-step
+output a PyMARL runner consumes written to HBM (positions, dones, t, reward,
+term, node/edge collisions, avail mask, window obs).  The timed path is the
+fused rollout kernel (`mapfx_rollout`, T steps per launch, state kept on
+chip); the per-step drop-in path (`mapfx_step`, one launch per step, state
+round-trips HBM) is measured too and reported under "per_step".
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "mapf-marl_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
+
+CONFIGS = {
+    # name: (H=W, N, envs per GPU, p_obstacle, shared warehouse map)
+    "c2": (32, 16, 4096, 0.10, False),
+    "c3": (64, 64, 2048, None, True),
+    "c5": (128, 256, 1024, 0.10, False),
+    "c1": (8, 2, 4096, 0.0, False),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=512)
+    ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--chunk", type=int, default=64, help="env steps per rollout launch")
+    ap.add_argument("--window", type=int, default=5)
+    ap.add_argument("--per-step-steps", type=int, default=200)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU work of the cpu_baseline sample (0 disables)")
+    ap.add_argument("--gather", action="store_true",
+                    help="also time the RCCL gather of (obs, reward, done) to rank 0")
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_c2.json"))
+    return ap.parse_args()
+
+
+def out_bytes_per_env_step(N, W):
+    """Algorithmic HBM bytes of one env step of the fused rollout:
+    actions N (read) + pos 8N + done N + t 4 + reward 8 + term 1 + node N + edge N
+    + avail N + window obs 2*W*W*N (written)."""
+    return N + 8 * N + N + 4 + 8 + 1 + N + N + N + 2 * W * W * N
+
+
+def canonical_bytes_per_env_step(H, Wd, N, W):
+    """SURVEY.md §8(d) D-4 canonical bytes of the per-step path (state round-trips
+    HBM): reads N + 8N + 8N + N + 4 + H*W/8, writes 8N + N + 4 + 8 + 2N + N + obs."""
+    return (N + 8 * N + 8 * N + N + 4 + (H * Wd) // 8) + (8 * N + N + 4 + 8 + 2 * N + N) \
+        + 2 * W * W * N
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import mapfx
+    from mapfx.maps import synthetic_instances, warehouse_grid
+
+    S, N, E, p, shared = CONFIGS[args.config]
+    W = args.window
+    K, WU, T = args.steps, args.warmup, args.chunk
+    if K % T or WU % T:
+        T = int(np.gcd(K, max(WU, T)) or 1)
+    offset = rank * E
+    inst = synthetic_instances(E, S, S, N, p_obstacle=p or 0.0, seed=1, env_offset=offset,
+                               shared_grid=warehouse_grid(S) if shared else None)
+    limit = 2 ** 31 - 1
+    b = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                            episode_limit=limit, obs=("window",), window=W,
+                            device="cuda:%d" % local, env_offset=offset, track_steps=False)
+    b.reset()
+    stream = torch.cuda.current_stream()
+    acts = b.gen_actions(WU + K, seed=2)                       # inputs resident in HBM
+    traj = b._alloc_out(T)
+    traj.pop("reward_f32")
+    outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done",
+            "traj_t")
+
+    def run_chunk(k0):
+        b.rollout(T, actions=acts[k0:k0 + T], traj=traj, outputs=outs)
+
+    # ---- warmup ----
+    for k0 in range(0, WU, T):
+        run_chunk(k0)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    # ---- timed: exactly K env steps of all envs ----
+    nl = K // T
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(nl)]
+    t0 = time.perf_counter()
+    for i in range(nl):
+        ev[i][0].record(stream)
+        run_chunk(WU + i * T)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kern_ms = float(np.mean([a.elapsed_time(c) for a, c in ev]))
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    total_envs = E * world
+    value = total_envs * N * K / elapsed           # agent-steps/s (agents x envs), whole job
+    bpes = out_bytes_per_env_step(N, W)
+    state_io = E * ((8 + 8 + 1) * N + 4 + inst["bits"].shape[1] * (0 if shared else 1)
+                    + (8 + 1) * N + 4)             # per-launch state read + write-back
+    launch_bytes = E * T * bpes + state_io
+    achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
+
+    # ---- per-step drop-in path (one mapfx_step launch per env step) ----
+    per_step = None
+    if args.per_step_steps > 0:
+        b2 = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                                 episode_limit=limit, obs=("window",), window=W,
+                                 device="cuda:%d" % local, env_offset=offset, track_steps=False)
+        b2.reset()
+        ks = args.per_step_steps
+        pouts = ("reward", "term", "node", "edge", "avail", "obs_window")
+        for k in range(min(20, ks)):
+            b2.step(acts[k], outputs=pouts)
+        torch.cuda.synchronize()
+        pev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(ks)]
+        t1 = time.perf_counter()
+        for k in range(ks):
+            pev[k][0].record(stream)
+            b2.step(acts[k % (WU + K)], outputs=pouts)
+            pev[k][1].record(stream)
+        torch.cuda.synchronize()
+        pel = time.perf_counter() - t1
+        pk_ms = float(np.mean([a.elapsed_time(c) for a, c in pev]))
+        cb = canonical_bytes_per_env_step(S, S, N, W)
+        per_step = {
+            "value": round(E * N * ks / pel * world, 1),
+            "ms_per_step": round(pel / ks * 1e3, 5),
+            "kernel_ms": round(pk_ms, 5),
+            "roofline": {"bound": "hbm", "achieved": round(E * cb / (pk_ms * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(E * cb / (pk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "bytes_per_env_step": cb},
+        }
+
+    # ---- optional RCCL gather of (obs, reward, done) to rank 0 ----
+    gather = None
+    if dist and args.gather:
+        gather = time_gather(dist, b, acts, traj, outs, T, WU, K, rank, world, E, N)
+
+    # ---- CPU baseline: the oracle's C restatement on this host (rank 0, N=1) ----
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(inst, S, N, E, W, args.cpu_seconds)
+
+    traffic = None
+    try:
+        with open(args.pmc) as f:
+            pm = json.load(f)
+        if pm.get("config") == args.config and pm.get("T") == T and pm.get("E") == E:
+            traffic = pm.get("traffic_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    if rank == 0:
+        line = {
+            "metric": "env-steps/sec (agents×envs) at 32×32/16-agent, 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "agent-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": WU,
+            "ms_per_step": round(elapsed / K * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32+f64",
+            "data": "synthetic (splitmix64 random maps p=%.2f, distinct free starts/goals, "
+                    "uniform random actions in HBM)" % (p or 0.0),
+            "config": {"workload": "%s: %dx%d grid, %d agents, %d envs/GPU, window %dx%d obs, "
+                                   "fused rollout T=%d" % (args.config, S, S, N, E, W, W, T),
+                       "envs_total": total_envs, "agents": N, "grid": [S, S],
+                       "parallelism": "env-shard x%d" % world},
+            "env_steps_per_s": round(total_envs * K / elapsed, 1),
+            "kernel_ms_per_launch": round(kern_ms, 5),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "bytes_per_env_step": bpes,
+                         "bytes_per_launch": int(launch_bytes)},
+            "per_step": per_step,
+            "cpu_baseline": cpu,
+        }
+        if gather is not None:
+            line["gather"] = gather
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def time_gather(dist, b, acts, traj, outs, T, WU, K, rank, world, E, N):
+    """Rollout chunks with the chunk's (window obs, reward, done) gathered to rank 0
+    over RCCL on a side stream, overlapped with the next chunk."""
+    side = torch.cuda.Stream()
+    bufs = [b._alloc_out(T), b._alloc_out(T)]
+    for bb in bufs:
+        bb.pop("reward_f32")
+    recv = None
+    if rank == 0:
+        recv = [[torch.empty_like(bufs[0][k]) for _ in range(world)]
+                for k in ("obs_window", "reward", "traj_done")]
+    nbytes = sum(bufs[0][k].numel() * bufs[0][k].element_size()
+                 for k in ("obs_window", "reward", "traj_done"))
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nl = K // T
+    ev_done = [torch.cuda.Event() for _ in range(2)]
+    for i in range(nl):
+        cur = bufs[i & 1]
+        if i >= 2:
+            torch.cuda.current_stream().wait_event(ev_done[i & 1])
+        b.rollout(T, actions=acts[WU + i * T:WU + (i + 1) * T], traj=cur, outputs=outs)
+        ready = torch.cuda.Event()
+        ready.record()
+        with torch.cuda.stream(side):
+            side.wait_event(ready)
+            for j, k in enumerate(("obs_window", "reward", "traj_done")):
+                dist.gather(cur[k], gather_list=recv[j] if rank == 0 else None, dst=0)
+            ev_done[i & 1].record(side)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    return {"value": round(world * E * N * K / el, 1), "ms_per_step": round(el / K * 1e3, 5),
+            "bytes_per_rank_per_chunk": int(nbytes), "chunk_steps": T,
+            "collective": "torch.distributed.gather (RCCL) to rank 0 on a side stream"}
+
+
+def cpu_baseline(inst, S, N, E, W, seconds):
+    """Time the oracle's bit-identical C restatement (OpenMP over envs) on a bounded
+    sample of the same workload: all envs of the shard, as many steps as fit in
+    ~`seconds` of CPU work.  Test infrastructure used only as the baseline."""
+    from oracle import corc
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=2 ** 31 - 1,
+                          nthreads=threads)
+    t0 = time.perf_counter()
+    ob.rollout(2, seed=2, t0=0, window=W)
+    probe = time.perf_counter() - t0
+    steps = int(max(1, min(2000, seconds / max(probe / 2, 1e-6))))
+    ob.reset()
+    t0 = time.perf_counter()
+    ob.rollout(steps, seed=2, t0=0, window=W)
+    el = time.perf_counter() - t0
+    return {"value": round(E * N * steps / el, 1), "unit": "agent-steps/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d envs x %d steps (%.1f s) of the same workload: oracle/mapf_oracle.c "
+                      "step + avail + window obs, OpenMP over envs" % (E, steps, el)}
+
+
+if __name__ == "__main__":
+    main()

@@ -194,8 +194,8 @@ __device__ inline void fill_map(const Geo& g, uint32_t* map32, const uint32_t* b
 // ---------------------------------------------------------------------------
 // The step kernel: T fused steps (T = 1 for mapfx_step; do_step = 0 observes).
 // ---------------------------------------------------------------------------
-template <typename CellT, int APL>
-__global__ void __launch_bounds__(256) mapf_step_kernel(Geo g, Args a) {
+template <typename CellT, int APL, bool ROLL>
+__device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   using CT = CellTraits<CellT>;
   extern __shared__ __align__(16) unsigned char lds[];
   const int tid = threadIdx.x;
@@ -264,7 +264,8 @@ __global__ void __launch_bounds__(256) mapf_step_kernel(Geo g, Args a) {
   const int es = (int)sizeof(CellT);  // obs element size == cell size
   const long long Elong = g.E;
 
-  for (int s = 0; s < a.T; ++s) {
+  const int T = ROLL ? a.T : 1;
+  for (int s = 0; s < T; ++s) {
     int* fl = flag + (s & 1) * 4;
     // ================= P0: move decision on the PRE-step map =================
     int oc[APL], nc[APL], act[APL], pre[APL];
@@ -326,7 +327,7 @@ __global__ void __launch_bounds__(256) mapf_step_kernel(Geo g, Args a) {
     if (a.do_step && !skip && env_ok) ++tcur;
     __syncthreads();  // B2: post-step map complete
     // ================= P2: collisions, rewards, avail, observations =================
-    const long long slotE = a.T > 1 ? (long long)s * Elong : 0;  // trajectory slot offset (envs)
+    const long long slotE = ROLL ? (long long)s * Elong : 0;  // trajectory slot offset (envs)
 #pragma unroll
     for (int k = 0; k < APL; ++k) {
       if (!has[k]) continue;
@@ -524,7 +525,7 @@ __global__ void __launch_bounds__(256) mapf_step_kernel(Geo g, Args a) {
       }
     }
     if (a.autoreset && alldone && a.do_step) tcur = 0;
-    if (s + 1 < a.T) __syncthreads();  // B4: map / staging reuse by the next step
+    if (ROLL && s + 1 < T) __syncthreads();  // B4: map / staging reuse by the next step
   }
 
   // ---- write back the env state ----
@@ -538,6 +539,18 @@ __global__ void __launch_bounds__(256) mapf_step_kernel(Geo g, Args a) {
     if (a.steps) a.steps[i] = st[k];
   }
   if (env_ok && lane == 0) a.t[env] = tcur;
+}
+
+// One env step (mapfx_step) or an observation pass (mapfx_observe, do_step = 0).
+template <typename CellT, int APL>
+__global__ void __launch_bounds__(256) mapf_step_kernel(Geo g, Args a) {
+  step_body<CellT, APL, false>(g, a);
+}
+
+// T fused env steps (mapfx_rollout); state stays in LDS / registers between steps.
+template <typename CellT, int APL>
+__global__ void __launch_bounds__(256) mapf_rollout_kernel(Geo g, Args a) {
+  step_body<CellT, APL, true>(g, a);
 }
 
 __global__ void reset_kernel(int E, int N, int32_t* pos, const int32_t* init_pos, uint8_t* done,
@@ -584,7 +597,17 @@ namespace {
 
 using KernelFn = void (*)(Geo, Args);
 
-KernelFn pick_kernel(int cell_bytes, int apl) {
+KernelFn pick_kernel(int cell_bytes, int apl, bool roll) {
+  if (roll) {
+    if (cell_bytes == 1) {
+      if (apl == 1) return mapf_rollout_kernel<uint8_t, 1>;
+      if (apl == 2) return mapf_rollout_kernel<uint8_t, 2>;
+      return mapf_rollout_kernel<uint8_t, 4>;
+    }
+    if (apl == 1) return mapf_rollout_kernel<uint16_t, 1>;
+    if (apl == 2) return mapf_rollout_kernel<uint16_t, 2>;
+    return mapf_rollout_kernel<uint16_t, 4>;
+  }
   if (cell_bytes == 1) {
     if (apl == 1) return mapf_step_kernel<uint8_t, 1>;
     if (apl == 2) return mapf_step_kernel<uint8_t, 2>;
@@ -600,14 +623,14 @@ int check_hip(hipError_t e, const char* what) {
   return MAPFX_OK;
 }
 
-int launch(mapfx_t* h, Args& a, hipStream_t stream) {
+int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream) {
   const Geo& g = h->geo;
   if (g.E == 0) return MAPFX_OK;
-  KernelFn fn = pick_kernel(h->cell_bytes, h->APL);
+  KernelFn fn = pick_kernel(h->cell_bytes, h->APL, roll);
   const int blocks = (g.E + g.EPB - 1) / g.EPB;
   const int lds = g.off_stage + g.EPB * g.stage_env_bytes;
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, g, a);
-  return check_hip(hipGetLastError(), "mapf_step_kernel launch");
+  return check_hip(hipGetLastError(), roll ? "mapf_rollout_kernel launch" : "mapf_step_kernel launch");
 }
 
 void fill_state_args(Args& a, const mapfx_state* st) {
@@ -801,9 +824,10 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
 
   const int lds_total = g.off_stage + EPB * g.stage_env_bytes;
   if (lds_total > 64 * 1024) {
-    KernelFn fn = pick_kernel(es, h->APL);
-    hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       lds_total);
+    hipError_t e = hipSuccess;
+    for (int roll = 0; roll < 2 && e == hipSuccess; ++roll)
+      e = hipFuncSetAttribute((const void*)pick_kernel(es, h->APL, roll != 0),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_total);
     if (e != hipSuccess) {
       delete h;
       return set_error(MAPFX_EHIP, "hipFuncSetAttribute(LDS=%d): %s", lds_total,
@@ -896,7 +920,7 @@ int mapfx_observe(mapfx_t* h, const mapfx_state* st, const mapfx_out* out, void*
   a.T = 1;
   a.do_step = 0;
   a.pow_lut = h->pow_lut;
-  return launch(h, a, (hipStream_t)stream);
+  return launch(h, a, false, (hipStream_t)stream);
 }
 
 int mapfx_step(mapfx_t* h, const mapfx_state* st, const void* actions, int action_dtype,
@@ -917,7 +941,7 @@ int mapfx_step(mapfx_t* h, const mapfx_state* st, const void* actions, int actio
   a.T = 1;
   a.do_step = 1;
   a.pow_lut = h->pow_lut;
-  return launch(h, a, (hipStream_t)stream);
+  return launch(h, a, false, (hipStream_t)stream);
 }
 
 int mapfx_rollout(mapfx_t* h, const mapfx_state* st, int32_t T, const void* actions,
@@ -944,7 +968,7 @@ int mapfx_rollout(mapfx_t* h, const mapfx_state* st, int32_t T, const void* acti
   a.autoreset = autoreset ? 1 : 0;
   a.do_step = 1;
   a.pow_lut = h->pow_lut;
-  return launch(h, a, (hipStream_t)stream);
+  return launch(h, a, true, (hipStream_t)stream);
 }
 
 int mapfx_gen_actions(mapfx_t* h, uint64_t seed, int32_t t0, int32_t T, int8_t* out,

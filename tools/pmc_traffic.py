@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 outputs of bench.py into profiles/.
+
+  python tools/pmc_traffic.py --trace DIR --fetch DIR --write DIR --out profiles/pmc_c2.json
+      [--kernel mapf_rollout_kernel] [--config c2 --T 64 --E 4096]
+
+* --trace: a `rocprofv3 --kernel-trace --stats --output-format csv` directory; the
+  per-kernel stats CSV is copied and the kernel's average duration recorded.
+* --fetch / --write: separate `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE`
+  passes (TCC FETCH_SIZE costs 3 of the 4 TCC slots, so they cannot share a pass).
+  Units are KB.  gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads
+  half of a wide coalesced stream's bytes, so it is doubled; WRITE_SIZE is taken
+  as is.  Per-launch HBM traffic = (2*FETCH_SIZE + WRITE_SIZE) * 1024 bytes,
+  averaged over the kernel's full-size dispatches.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import statistics
+
+
+def _rows(d, pattern):
+    out = []
+    for p in glob.glob(os.path.join(d, "**", pattern), recursive=True):
+        with open(p, newline="") as f:
+            out.extend(csv.DictReader(f))
+    return out
+
+
+def _col(row, *names):
+    for n in names:
+        if n in row:
+            return row[n]
+    raise KeyError(names)
+
+
+def pmc_values(d, kernel, counter):
+    per_dispatch = {}
+    for r in _rows(d, "*counter_collection.csv"):
+        if kernel not in _col(r, "Kernel_Name", "KernelName"):
+            continue
+        if _col(r, "Counter_Name", "CounterName") != counter:
+            continue
+        did = _col(r, "Dispatch_Id", "DispatchId", "Correlation_Id")
+        per_dispatch[did] = per_dispatch.get(did, 0.0) + float(_col(r, "Counter_Value",
+                                                                     "CounterValue"))
+    vals = sorted(per_dispatch.values())
+    if not vals:
+        return None, 0
+    big = [v for v in vals if v >= 0.5 * vals[-1]]  # full-size launches only
+    return statistics.mean(big), len(big)
+
+
+def trace_stats(d, kernel, out_dir, tag):
+    stats = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+    res = {}
+    for p in stats:
+        dst = os.path.join(out_dir, "%s_kernel_stats.csv" % tag)
+        shutil.copy(p, dst)
+        res["stats_csv"] = os.path.relpath(dst, os.path.dirname(out_dir))
+        with open(p, newline="") as f:
+            for r in csv.DictReader(f):
+                name = _col(r, "Name", "KERNEL_NAME", "Kernel_Name")
+                if kernel in name:
+                    res.setdefault("kernels", []).append({
+                        "name": name[:160], "calls": int(float(_col(r, "Calls"))),
+                        "avg_ns": float(_col(r, "AverageNs", "Average_Ns")),
+                        "total_ns": float(_col(r, "TotalDurationNs", "Total_Duration_Ns"))})
+    # per-dispatch durations from the kernel trace
+    durs = []
+    for r in _rows(d, "*kernel_trace.csv"):
+        if kernel in _col(r, "Kernel_Name", "KernelName"):
+            durs.append(int(_col(r, "End_Timestamp")) - int(_col(r, "Start_Timestamp")))
+    if durs:
+        res["dispatches"] = len(durs)
+        res["median_ns"] = statistics.median(durs)
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace")
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--kernel", default="mapf_rollout_kernel")
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--T", type=int, default=64)
+    ap.add_argument("--E", type=int, default=4096)
+    ap.add_argument("--tag", default="r01_c2")
+    a = ap.parse_args()
+    out_dir = os.path.dirname(os.path.abspath(a.out))
+    os.makedirs(out_dir, exist_ok=True)
+    res = {"config": a.config, "T": a.T, "E": a.E, "kernel": a.kernel}
+    if a.trace:
+        res["trace"] = trace_stats(a.trace, a.kernel, out_dir, a.tag)
+    fetch = write = None
+    if a.fetch:
+        fetch, nf = pmc_values(a.fetch, a.kernel, "FETCH_SIZE")
+        res["FETCH_SIZE_kb"] = fetch
+        res["fetch_dispatches"] = nf
+    if a.write:
+        write, nw = pmc_values(a.write, a.kernel, "WRITE_SIZE")
+        res["WRITE_SIZE_kb"] = write
+        res["write_dispatches"] = nw
+    if fetch is not None and write is not None:
+        res["traffic_bytes_per_launch"] = int((2.0 * fetch + write) * 1024)
+        res["traffic_note"] = "(2*FETCH_SIZE + WRITE_SIZE)*1024: gfx950 FETCH_SIZE halving corrected"
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -92,6 +92,10 @@ struct Geo {
   int obs_mode;
   int limit;
   double step_rew, collide_rew;
+  // wave-local fast path (N <= 64: an env never spans two wavefronts)
+  int wave_ok, EPW;
+  int wv_off_map, wv_off_who, wv_off_bits, wv_off_rew, wv_off_stage, wv_lds;
+  int who_env_bytes, wv_bits_env_bytes;
 };
 
 struct Args {
@@ -541,6 +545,322 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   if (env_ok && lane == 0) a.t[env] = tcur;
 }
 
+
+// ===========================================================================
+// Wave-local fast path (N <= 64).  Every env lives inside ONE wavefront
+// (L = pow2ceil(N) lanes, 64/L envs per wave), so a step needs no workgroup
+// barrier at all: LDS instructions of a wave execute in order, and cross-lane
+// values move with ds_bpermute (__shfl) or wave ballots.  Blocks are one wave;
+// waves never wait on each other.  Per step, per agent lane:
+//   1 LDS read (candidate cell) -> 2 LDS atomics (move the count) -> 1 LDS read
+//   (node) -> [who-map lookup + bpermute only for agents that moved into a
+//   pre-occupied cell] -> 4 LDS reads (avail) -> WIN x ds_read2 + SWAR (window)
+//   -> u16 staging writes; one lane per env folds the fp64 rewards in agent order.
+// Actions for step s+1 are loaded while step s runs.
+// ===========================================================================
+__device__ inline void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 4 padded-map cells (one u32, bytes = obstacle flag 0x80 | count) ->
+// obstacle plane bytes and agents plane bytes of the marl_partial window.
+__device__ inline void swar_window(uint32_t v, uint32_t& ob, uint32_t& ag) {
+  const uint32_t f = (v >> 7) & 0x01010101u;
+  const uint32_t cnt = v & 0x7F7F7F7Fu;
+  const uint32_t nz = ((cnt + 0x7F7F7F7Fu) >> 7) & 0x01010101u;  // 1 where count >= 1
+  ob = f & (nz ^ 0x01010101u);                                     // occ == -1
+  ag = cnt - (f & nz);                                             // max(occ, 0)
+}
+
+__device__ inline int load_action_w(const Args& a, long long idx) {
+  return load_action(a.actions, a.act_dtype, idx);
+}
+
+template <int WIN, bool ROLL>
+__global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  const int lane64 = threadIdx.x;
+  const int slot = lane64 >> g.lshift;       // env slot within the wave
+  const int ag = lane64 & (g.L - 1);         // agent index
+  const int base = slot << g.lshift;         // first lane of this env
+  const int env0 = blockIdx.x * g.EPW;
+  const int env = env0 + slot;
+  const int N = g.N;
+  const bool has = env < g.E && ag < N;
+  const bool env_ok = env < g.E;
+  const uint64_t envmask = (g.L == 64 ? ~0ull : ((1ull << g.L) - 1ull)) << base;
+
+  unsigned char* map = lds + g.wv_off_map + slot * g.map_env_bytes;
+  uint32_t* map32 = (uint32_t*)map;
+  unsigned char* who = lds + g.wv_off_who + slot * g.who_env_bytes;
+  uint32_t* bitsL = (uint32_t*)(lds + g.wv_off_bits + slot * g.wv_bits_env_bytes);
+  double* rew = (double*)(lds + g.wv_off_rew) + slot * N;
+  unsigned char* stage = lds + g.wv_off_stage;  // [EPW][N][2][WIN][WIN]
+
+  int r = 0, c = 0, gr = 0, gc = 0, st = 0;
+  bool dn = false;
+  const long long ia = (long long)env * N + ag;
+  if (has) {
+    const int2 p = ((const int2*)a.pos)[ia];
+    const int2 q = ((const int2*)a.goal)[ia];
+    r = p.x;
+    c = p.y;
+    gr = q.x;
+    gc = q.y;
+    dn = a.done[ia] != 0;
+    if (a.steps) st = a.steps[ia];
+  }
+  int tcur = env_ok ? a.t[env] : 0;
+  const int T = ROLL ? a.T : 1;
+  const long long Elong = g.E;
+  // first action (prefetch)
+  int act_next = 4;
+  if (has && a.do_step) {
+    act_next = a.use_rng ? gen_action(a.seed, g.env_offset + env, a.t0, ag)
+                         : load_action_w(a, (long long)env * N + ag);
+  }
+
+  // ---- bitmap -> LDS, padded map, agents, who map ----
+  if (env_ok) {
+    const uint32_t* src =
+        (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)env * g.map_stride));
+    for (int w = ag; w < g.bits_words; w += g.L) bitsL[w] = src[w];
+  }
+  wave_fence();
+  for (int wi = ag; wi < g.map_words; wi += g.L) {
+    const int pr = fastdiv(wi, g.m_wpr);
+    const int pw = wi - pr * g.wpr;
+    const int rr = pr - g.P;
+    const int c0 = pw * 4 - g.pl;
+    uint32_t word = 0x80808080u;
+    if (rr >= 0 && rr < g.H && c0 >= 0 && c0 < g.W) {
+      const int p = rr * g.W + c0;
+      const uint32_t w0 = bitsL[p >> 5], w1 = bitsL[(p >> 5) + 1];
+      uint32_t nib = __builtin_amdgcn_alignbit(w1, w0, p & 31) & 0xFu;
+      if (c0 + 4 > g.W) nib |= (0xFu << (g.W - c0)) & 0xFu;  // right border cells
+      word = ((nib * 0x00204081u) & 0x01010101u) * 0x80u;
+    }
+    map32[wi] = word;
+  }
+  wave_fence();
+  int oc = (r + g.P) * g.pitch + c + g.pl;
+  if (has) {
+    atomicAdd(&map32[oc >> 2], 1u << ((oc & 3) * 8));
+    who[r * g.W + c] = (unsigned char)ag;
+  }
+  wave_fence();
+
+  for (int s = 0; s < T; ++s) {
+    const long long slotE = ROLL ? (long long)s * Elong : 0;
+    const int act = act_next;
+    if (ROLL && s + 1 < T && has && a.do_step) {  // prefetch the next step's action
+      act_next = a.use_rng ? gen_action(a.seed, g.env_offset + env, a.t0 + s + 1, ag)
+                           : load_action_w(a, ((long long)(s + 1) * Elong + env) * N + ag);
+    }
+    // ---------------- move decision on the PRE-step map ----------------
+    oc = (r + g.P) * g.pitch + c + g.pl;
+    int nc = oc, pre = 0, av = act;
+    bool moved = false, envc = false;
+    const bool bad_l = has && a.do_step && (act < 0 || act > 4);
+    if (bad_l) av = 4;
+    if (has && a.do_step && !dn && av != 4) {  // __agent_step :319-342
+      const int cand = oc + (av == 0 ? -g.pitch : (av == 1 ? g.pitch : (av == 2 ? -1 : 1)));
+      const uint32_t v = map[cand];
+      if (v == 0x80u) {
+        envc = true;
+      } else {
+        nc = cand;
+        moved = true;
+        pre = (int)(v & 0x7Fu);
+      }
+    }
+    const bool skip = !a.do_step || ((__ballot(bad_l) & envmask) != 0);
+    if (skip) {
+      nc = oc;
+      moved = envc = false;
+    }
+    if (moved) {
+      atomicSub(&map32[oc >> 2], 1u << ((oc & 3) * 8));
+      atomicAdd(&map32[nc >> 2], 1u << ((nc & 3) * 8));
+      r += act_dr(av);
+      c += act_dc(av);
+    }
+    wave_fence();
+    // ---------------- collisions + reward ----------------
+    int node = 0, edge = 0;
+    if (a.do_step && !skip) {
+      node = ((uint32_t)map[nc] & 0x7Fu) > 1u ? 1 : 0;  // :344-362
+    }
+    const bool suspect = moved && pre > 0;  // edge needs j with old_j == new_i (:364-383)
+    if (__ballot(suspect)) {
+      // pre == 1: the unique pre-step occupant is who[new cell]
+      const int jw = suspect ? (int)who[r * g.W + c] : 0;
+      const int oj = __shfl(oc, base + jw);
+      const int nj = __shfl(nc, base + jw);
+      if (suspect && pre == 1) edge = (nj == oc && oj == nc) ? 1 : 0;
+      if (__ballot(suspect && pre > 1)) {  // stacked pre-occupants: scan the env
+        for (int j = 0; j < N; ++j) {
+          const int oj2 = __shfl(oc, base + j);
+          const int nj2 = __shfl(nc, base + j);
+          if (suspect && pre > 1) edge += (oj2 == nc) & (nj2 == oc);
+        }
+      }
+    }
+    if (has && a.do_step && !skip) {
+      double rr = 0.0;  // :94-130, exact fp64 op order
+      if (!dn) {
+        if (envc) rr = rr + g.collide_rew;
+        rr = rr + g.step_rew;
+        ++st;
+      }
+      rr = rr + g.collide_rew * (double)node;
+      rr = rr + g.collide_rew * (double)edge;
+      rew[ag] = rr;
+      if (r == gr && c == gc) dn = true;   // :112-114
+      if (tcur + 1 >= g.limit) dn = true;  // :116-117 (t already incremented below)
+    } else if (has && a.do_step) {
+      rew[ag] = 0.0;
+    }
+    if (a.do_step && !skip) ++tcur;
+    // who map for the next step (post-step positions); after every read above
+    if (has) who[r * g.W + c] = (unsigned char)ag;
+    const bool alldone = (__ballot(has && !dn) & envmask) == 0;
+    // ---------------- per-agent outputs ----------------
+    if (has) {
+      const long long ai = (slotE + env) * N + ag;
+      if (a.do_step) {
+        if (a.node) a.node[ai] = (uint8_t)node;
+        if (a.edge) a.edge[ai] = (uint8_t)(edge > 255 ? 255 : edge);
+      }
+      if (a.traj_pos) ((int2*)a.traj_pos)[ai] = make_int2(r, c);
+      if (a.traj_done) a.traj_done[ai] = dn ? 1 : 0;
+      if (a.avail) {  // :203-224 on the post-step map
+        uint32_t m = 16u;
+        m |= (map[nc - g.pitch] != 0x80u) ? 1u : 0u;
+        m |= (map[nc + g.pitch] != 0x80u) ? 2u : 0u;
+        m |= (map[nc - 1] != 0x80u) ? 4u : 0u;
+        m |= (map[nc + 1] != 0x80u) ? 8u : 0u;
+        a.avail[ai] = (uint8_t)m;
+      }
+    }
+    if (WIN > 0 && a.obs_window) {  // marl_partial.py:323-342 via SWAR, staged as u16
+      if (has) {
+        constexpr int WW = WIN * WIN;
+        constexpr int H2 = WIN / 2;
+        // bytes of the agent's record: [obstacle WxW][agents WxW], 2*WW bytes
+        uint32_t ob[(WW + 3) / 4 + 1], agb[(WW + 3) / 4 + 1];
+#pragma unroll
+        for (int k = 0; k < (WW + 3) / 4 + 1; ++k) ob[k] = agb[k] = 0;
+#pragma unroll
+        for (int y = 0; y < WIN; ++y) {
+          const int a0 = nc + (y - H2) * g.pitch - H2;  // first cell of the row
+          const int wb = a0 >> 2, o = a0 & 3;
+          const uint32_t lo = map32[wb], hi = map32[wb + 1];
+          uint32_t hi2 = 0;
+          if (WIN > 5) hi2 = map32[wb + 2];
+          // cells a0 .. a0+WIN-1 as bytes
+          const uint32_t x0 = __builtin_amdgcn_alignbyte(hi, lo, o);
+          const uint32_t x1 = __builtin_amdgcn_alignbyte(hi2, hi, o);
+          uint32_t o0, g0, o1, g1;
+          swar_window(x0, o0, g0);
+          swar_window(x1, o1, g1);
+          // append WIN bytes at byte offset y*WIN of each plane
+#pragma unroll
+          for (int x = 0; x < WIN; ++x) {
+            const uint32_t bo = x < 4 ? (o0 >> (8 * x)) & 0xFFu : (o1 >> (8 * (x - 4))) & 0xFFu;
+            const uint32_t bg = x < 4 ? (g0 >> (8 * x)) & 0xFFu : (g1 >> (8 * (x - 4))) & 0xFFu;
+            const int q = y * WIN + x;  // compile-time
+            ob[q >> 2] |= bo << (8 * (q & 3));
+            agb[q >> 2] |= bg << (8 * (q & 3));
+          }
+        }
+        // record bytes: b[k] = k < WW ? ob-byte k : agb-byte (k - WW); written as u16
+        unsigned char* dst = stage + (size_t)(slot * N + ag) * 2 * WW;
+#pragma unroll
+        for (int k = 0; k < WW; ++k) {
+          const int k0 = 2 * k, k1 = 2 * k + 1;
+          const uint32_t b0 = k0 < WW ? (ob[k0 >> 2] >> (8 * (k0 & 3))) & 0xFFu
+                                      : (agb[(k0 - WW) >> 2] >> (8 * ((k0 - WW) & 3))) & 0xFFu;
+          const uint32_t b1 = k1 < WW ? (ob[k1 >> 2] >> (8 * (k1 & 3))) & 0xFFu
+                                      : (agb[(k1 - WW) >> 2] >> (8 * ((k1 - WW) & 3))) & 0xFFu;
+          *(uint16_t*)(dst + k0) = (uint16_t)(b0 | (b1 << 8));
+        }
+      }
+    }
+    if (a.obs_full && env_ok) {  // :143-192, row-major occ = count - flag
+      unsigned char* outb = (unsigned char*)a.obs_full + (slotE + env) * (long long)g.H * g.W;
+      if ((g.W & 3) == 0) {
+        const int wpr_out = g.W >> 2;
+        const int nwords = g.H * wpr_out;
+        for (int i = ag; i < nwords; i += g.L) {
+          const int rr_ = fastdiv(i, g.m_W4);
+          const int cw = i - rr_ * wpr_out;
+          const uint32_t v = map32[((rr_ + g.P) * g.pitch + g.pl) / 4 + cw];
+          const uint32_t f = (v >> 7) & 0x01010101u;
+          ((uint32_t*)outb)[i] = (((v & 0x7F7F7F7Fu) | 0x80808080u) - f) ^ 0x80808080u;
+        }
+      } else {
+        for (int i = ag; i < g.H * g.W; i += g.L) {
+          const int rr_ = fastdiv(i, g.m_W);
+          const int cc_ = i - rr_ * g.W;
+          const uint32_t v = map[(rr_ + g.P) * g.pitch + cc_ + g.pl];
+          ((int8_t*)outb)[i] = (int8_t)((int)(v & 0x7Fu) - (int)(v >> 7));
+        }
+      }
+    }
+    wave_fence();
+    // ---------------- env outputs: fp64 fold in agent order (:141) ----------------
+    if (env_ok && ag == 0) {
+      if (a.do_step) {
+        double R = 0.0;
+        for (int j = 0; j < N; ++j) R = R + rew[j];
+        if (a.reward) a.reward[slotE + env] = R;
+        if (a.reward_f32) a.reward_f32[slotE + env] = (float)R;
+        if (a.err && skip) atomicCAS(a.err, 0, env + 1);
+      }
+      if (a.term) a.term[slotE + env] = alldone ? 1 : 0;
+      if (a.traj_t) a.traj_t[slotE + env] = tcur;
+    }
+    if (WIN > 0 && a.obs_window) {  // staging -> HBM, 16 B per lane
+      const int nenv = min(g.EPW, g.E - env0);
+      const long long bytes = (long long)nenv * N * 2 * WIN * WIN;
+      unsigned char* dst =
+          (unsigned char*)a.obs_window + (slotE + env0) * (long long)N * 2 * WIN * WIN;
+      if ((((uintptr_t)dst) & 15) == 0 && (bytes & 15) == 0) {
+        for (long long i = lane64; i < (bytes >> 4); i += 64)
+          ((uint4*)dst)[i] = ((const uint4*)stage)[i];
+      } else {
+        for (long long i = lane64; i < bytes; i += 64) dst[i] = stage[i];
+      }
+    }
+    if (ROLL && a.autoreset && a.do_step && alldone && has) {
+      const int2 p = ((const int2*)a.init_pos)[ia];
+      const int ocell = (r + g.P) * g.pitch + c + g.pl;
+      const int ncell = (p.x + g.P) * g.pitch + p.y + g.pl;
+      atomicSub(&map32[ocell >> 2], 1u << ((ocell & 3) * 8));
+      atomicAdd(&map32[ncell >> 2], 1u << ((ncell & 3) * 8));
+      r = p.x;
+      c = p.y;
+      dn = false;
+      st = 0;
+    }
+    if (ROLL && a.autoreset && a.do_step && alldone) {
+      tcur = 0;
+      wave_fence();
+      if (has) who[r * g.W + c] = (unsigned char)ag;
+    }
+    wave_fence();
+  }
+  if (has) {
+    ((int2*)a.pos)[ia] = make_int2(r, c);
+    a.done[ia] = dn ? 1 : 0;
+    if (a.steps) a.steps[ia] = st;
+  }
+  if (env_ok && ag == 0) a.t[env] = tcur;
+}
+
 // One env step (mapfx_step) or an observation pass (mapfx_observe, do_step = 0).
 template <typename CellT, int APL>
 __global__ void __launch_bounds__(256) mapf_step_kernel(Geo g, Args a) {
@@ -623,9 +943,37 @@ int check_hip(hipError_t e, const char* what) {
   return MAPFX_OK;
 }
 
+KernelFn pick_wave_kernel(int win, bool roll) {
+  if (roll) {
+    switch (win) {
+      case 0: return mapf_wave_kernel<0, true>;
+      case 3: return mapf_wave_kernel<3, true>;
+      case 5: return mapf_wave_kernel<5, true>;
+      case 7: return mapf_wave_kernel<7, true>;
+    }
+  } else {
+    switch (win) {
+      case 0: return mapf_wave_kernel<0, false>;
+      case 3: return mapf_wave_kernel<3, false>;
+      case 5: return mapf_wave_kernel<5, false>;
+      case 7: return mapf_wave_kernel<7, false>;
+    }
+  }
+  return nullptr;
+}
+
 int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream) {
   const Geo& g = h->geo;
   if (g.E == 0) return MAPFX_OK;
+  // wave-local fast path: N <= 64, no PRIMAL output, window 3/5/7 (or none)
+  if (g.wave_ok && !a.obs_primal && !a.primal_vec) {
+    KernelFn fn = pick_wave_kernel(a.obs_window ? g.window : 0, roll);
+    if (fn) {
+      const int blocks = (g.E + g.EPW - 1) / g.EPW;
+      hipLaunchKernelGGL(fn, dim3(blocks), dim3(64), g.wv_lds, stream, g, a);
+      return check_hip(hipGetLastError(), "mapf_wave_kernel launch");
+    }
+  }
   KernelFn fn = pick_kernel(h->cell_bytes, h->APL, roll);
   const int blocks = (g.E + g.EPB - 1) / g.EPB;
   const int lds = g.off_stage + g.EPB * g.stage_env_bytes;
@@ -821,6 +1169,28 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   g.off_flag = off;
   off += round_up(EPB * 8 * 4, 16);
   g.off_stage = off;
+
+  // wave-local fast path layout (one wavefront = EPW envs)
+  g.wave_ok = 0;
+  if (L <= 64 && es == 1) {
+    const int EPW = 64 / L;
+    g.EPW = EPW;
+    g.who_env_bytes = round_up(c.H * c.W, 16);
+    g.wv_bits_env_bytes = round_up(g.bits_words * 4 + 4, 16);
+    int o = 0;
+    g.wv_off_map = o;
+    o += EPW * g.map_env_bytes;
+    g.wv_off_who = o;
+    o += EPW * g.who_env_bytes;
+    g.wv_off_bits = o;
+    o += EPW * g.wv_bits_env_bytes;
+    g.wv_off_rew = o;
+    o += round_up(EPW * N * 8, 16);
+    g.wv_off_stage = o;
+    o += EPW * g.stage_env_bytes;
+    g.wv_lds = o;
+    g.wave_ok = (o <= 64 * 1024) ? 1 : 0;
+  }
 
   const int lds_total = g.off_stage + EPB * g.stage_env_bytes;
   if (lds_total > 64 * 1024) {

@@ -162,14 +162,21 @@ def test_batched_primal_matches_oracle(mapfx_mod, S, N, s, E):
 # ---------------------------------------------------------------------------
 # 3. fused rollout == repeated steps; device generator == host generator
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("S,N,E,T", [(32, 16, 1000, 20), (8, 2, 300, 50), (64, 64, 40, 8),
-                                     (128, 256, 4, 4)])
-def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T):
+@pytest.mark.parametrize("S,N,E,T,obs,win", [
+    (32, 16, 1000, 20, ("full", "window", "primal"), 5),   # generic kernel (PRIMAL)
+    (32, 16, 1000, 20, ("full", "window"), 5),             # wave-local fast path
+    (8, 2, 300, 50, ("full", "window"), 3),
+    (13, 7, 200, 30, ("full", "window"), 7),
+    (8, 2, 300, 50, ("full", "window", "primal"), 5),
+    (64, 64, 40, 8, ("full", "window"), 5),
+    (64, 64, 40, 8, ("full", "window", "primal"), 5),
+    (128, 256, 4, 4, ("full", "window", "primal"), 5)])
+def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T, obs, win):
     from mapfx import rng
     from mapfx.maps import synthetic_instances
     inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=5)
-    kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=35, obs=("full", "window", "primal"),
-              window=5, primal_size=10)
+    kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=35, obs=obs, window=win,
+              primal_size=10)
     b1 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], env_offset=1000, **kw)
     b2 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], env_offset=1000, **kw)
     b1.reset()
@@ -186,6 +193,8 @@ def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T):
         out = b3.step(acts[k])
         for key in ("reward", "node", "edge", "avail", "term", "obs_full", "obs_window",
                     "obs_primal", "primal_vec"):
+            if key not in out:
+                continue
             x = _np(out[key])
             for tr in (traj, traj_buf):
                 y = _np(tr[key][k])

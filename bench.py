@@ -287,7 +287,7 @@ def cpu_baseline(inst, S, N, E, W, seconds):
     t0 = time.perf_counter()
     ob.rollout(2, seed=2, t0=0, window=W)
     probe = time.perf_counter() - t0
-    steps = int(max(1, min(2000, seconds / max(probe / 2, 1e-6))))
+    steps = int(max(1, min(200000, seconds / max(probe / 2, 1e-6))))
     ob.reset()
     t0 = time.perf_counter()
     ob.rollout(steps, seed=2, t0=0, window=W)

@@ -552,11 +552,14 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
 // barrier at all: LDS instructions of a wave execute in order, and cross-lane
 // values move with ds_bpermute (__shfl) or wave ballots.  Blocks are one wave;
 // waves never wait on each other.  Per step, per agent lane:
-//   1 LDS read (candidate cell) -> 2 LDS atomics (move the count) -> 1 LDS read
-//   (node) -> [who-map lookup + bpermute only for agents that moved into a
-//   pre-occupied cell] -> 4 LDS reads (avail) -> WIN x ds_read2 + SWAR (window)
-//   -> u16 staging writes; one lane per env folds the fp64 rewards in agent order.
-// Actions for step s+1 are loaded while step s runs.
+//   1 LDS read (candidate cell, PRE-step map) -> 2 LDS atomics (move the count)
+//   -> WIN row reads of the POST-step map, turned by SWAR into the window's
+//   obstacle / agents planes; node collision and avail fall out of the same
+//   rows -> who-map lookup + bpermute only for agents that moved into a
+//   pre-occupied cell (edge collisions) -> the 2*WIN*WIN-byte record is packed
+//   in registers and staged as u16; one lane per env folds the fp64 rewards in
+//   agent order; the wave writes the staged records with 16-byte stores.
+// Actions for step s+1 are loaded while step s runs.  All offsets are 32-bit.
 // ===========================================================================
 __device__ inline void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -565,62 +568,85 @@ __device__ inline void wave_fence() {
 }
 
 // 4 padded-map cells (one u32, bytes = obstacle flag 0x80 | count) ->
-// obstacle plane bytes and agents plane bytes of the marl_partial window.
+// obstacle plane bytes (occ == -1) and agents plane bytes (max(occ, 0)).
 __device__ inline void swar_window(uint32_t v, uint32_t& ob, uint32_t& ag) {
   const uint32_t f = (v >> 7) & 0x01010101u;
   const uint32_t cnt = v & 0x7F7F7F7Fu;
   const uint32_t nz = ((cnt + 0x7F7F7F7Fu) >> 7) & 0x01010101u;  // 1 where count >= 1
-  ob = f & (nz ^ 0x01010101u);                                     // occ == -1
-  ag = cnt - (f & nz);                                             // max(occ, 0)
+  ob = f & (nz ^ 0x01010101u);
+  ag = cnt - (f & nz);
 }
 
-__device__ inline int load_action_w(const Args& a, long long idx) {
-  return load_action(a.actions, a.act_dtype, idx);
+// OR a chunk of `bits` (<= 56) bits into a little-endian u64 bit stream at `pos`
+// (all arguments compile-time after unrolling).
+template <int NW>
+__device__ __forceinline__ void put_bits(uint64_t (&w)[NW], int pos, int bits, uint64_t chunk) {
+  const int wi = pos >> 6, sh = pos & 63;
+  w[wi] |= chunk << sh;
+  if (sh + bits > 64 && wi + 1 < NW) w[wi + 1] |= chunk >> (64 - sh);
 }
 
-template <int WIN, bool ROLL>
+// Byte b of the packed window record held in registers: obstacle plane
+// (rows o0[y]: cols 0-3, o1[y]: col 4-7), then agents plane (g0[y], g1[y]).
+template <int WIN>
+__device__ __forceinline__ uint32_t rec_byte(int b, const uint32_t* o0, const uint32_t* o1,
+                                             const uint32_t* g0, const uint32_t* g1) {
+  constexpr int WW = WIN * WIN;
+  const int pl = b / WW, q = b % WW, y = q / WIN, x = q % WIN;
+  const uint32_t src = pl == 0 ? (x < 4 ? o0[y] : o1[y]) : (x < 4 ? g0[y] : g1[y]);
+  return (src >> (8 * (x & 3))) & 0xFFu;
+}
+
+// FULLW: every lane owns an agent (N == L and E % EPW == 0) -> no lane masks.
+// RUNNER (rollout only): the standard runner outputs are all present (reward,
+// term, node, edge, avail, traj_pos/done/t, window obs) -> no per-output tests.
+template <int WIN, bool ROLL, bool FULLW, bool RUNNER>
 __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   extern __shared__ __align__(16) unsigned char lds[];
+  constexpr int WW = WIN * WIN;
+  constexpr int H2 = WIN / 2;
+  constexpr int REC = 2 * WW;  // record bytes per agent
   const int lane64 = threadIdx.x;
-  const int slot = lane64 >> g.lshift;       // env slot within the wave
-  const int ag = lane64 & (g.L - 1);         // agent index
-  const int base = slot << g.lshift;         // first lane of this env
+  const int slot = lane64 >> g.lshift;  // env slot within the wave
+  const int ag = lane64 & (g.L - 1);    // agent index
+  const int base = slot << g.lshift;    // first lane of this env
   const int env0 = blockIdx.x * g.EPW;
   const int env = env0 + slot;
   const int N = g.N;
-  const bool has = env < g.E && ag < N;
-  const bool env_ok = env < g.E;
+  const bool env_ok = FULLW || env < g.E;
+  const bool has = FULLW || (env_ok && ag < N);
+  const bool do_step = ROLL || a.do_step;
   const uint64_t envmask = (g.L == 64 ? ~0ull : ((1ull << g.L) - 1ull)) << base;
+  const int pitch = g.pitch;
+  const int Wd = g.W;
 
   unsigned char* map = lds + g.wv_off_map + slot * g.map_env_bytes;
   uint32_t* map32 = (uint32_t*)map;
   unsigned char* who = lds + g.wv_off_who + slot * g.who_env_bytes;
   uint32_t* bitsL = (uint32_t*)(lds + g.wv_off_bits + slot * g.wv_bits_env_bytes);
   double* rew = (double*)(lds + g.wv_off_rew) + slot * N;
-  unsigned char* stage = lds + g.wv_off_stage;  // [EPW][N][2][WIN][WIN]
+  unsigned char* stage = lds + g.wv_off_stage;  // [EPW][N][REC]
 
+  const uint32_t oa = (uint32_t)(env * N + ag);  // agent index inside one step slot
+  const uint32_t EN = (uint32_t)(g.E * N);
   int r = 0, c = 0, gr = 0, gc = 0, st = 0;
   bool dn = false;
-  const long long ia = (long long)env * N + ag;
   if (has) {
-    const int2 p = ((const int2*)a.pos)[ia];
-    const int2 q = ((const int2*)a.goal)[ia];
+    const int2 p = ((const int2*)a.pos)[oa];
+    const int2 q = ((const int2*)a.goal)[oa];
     r = p.x;
     c = p.y;
     gr = q.x;
     gc = q.y;
-    dn = a.done[ia] != 0;
-    if (a.steps) st = a.steps[ia];
+    dn = a.done[oa] != 0;
+    if (a.steps) st = a.steps[oa];
   }
   int tcur = env_ok ? a.t[env] : 0;
   const int T = ROLL ? a.T : 1;
-  const long long Elong = g.E;
-  // first action (prefetch)
-  int act_next = 4;
-  if (has && a.do_step) {
-    act_next = a.use_rng ? gen_action(a.seed, g.env_offset + env, a.t0, ag)
-                         : load_action_w(a, (long long)env * N + ag);
-  }
+  // Actions are fetched for AB steps at a time: one VMEM wait per block instead of
+  // one per step (a wait on a per-step load would also drain the step's stores).
+  constexpr int AB = ROLL ? 16 : 1;
+  uint32_t actpk[(AB + 3) / 4];
 
   // ---- bitmap -> LDS, padded map, agents, who map ----
   if (env_ok) {
@@ -635,68 +661,83 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
     const int rr = pr - g.P;
     const int c0 = pw * 4 - g.pl;
     uint32_t word = 0x80808080u;
-    if (rr >= 0 && rr < g.H && c0 >= 0 && c0 < g.W) {
-      const int p = rr * g.W + c0;
+    if (rr >= 0 && rr < g.H && c0 >= 0 && c0 < Wd) {
+      const int p = rr * Wd + c0;
       const uint32_t w0 = bitsL[p >> 5], w1 = bitsL[(p >> 5) + 1];
       uint32_t nib = __builtin_amdgcn_alignbit(w1, w0, p & 31) & 0xFu;
-      if (c0 + 4 > g.W) nib |= (0xFu << (g.W - c0)) & 0xFu;  // right border cells
+      if (c0 + 4 > Wd) nib |= (0xFu << (Wd - c0)) & 0xFu;  // right border cells
       word = ((nib * 0x00204081u) & 0x01010101u) * 0x80u;
     }
     map32[wi] = word;
   }
   wave_fence();
-  int oc = (r + g.P) * g.pitch + c + g.pl;
   if (has) {
+    const int oc = (r + g.P) * pitch + c + g.pl;
     atomicAdd(&map32[oc >> 2], 1u << ((oc & 3) * 8));
-    who[r * g.W + c] = (unsigned char)ag;
+    who[r * Wd + c] = (unsigned char)ag;
   }
   wave_fence();
 
   for (int s = 0; s < T; ++s) {
-    const long long slotE = ROLL ? (long long)s * Elong : 0;
-    const int act = act_next;
-    if (ROLL && s + 1 < T && has && a.do_step) {  // prefetch the next step's action
-      act_next = a.use_rng ? gen_action(a.seed, g.env_offset + env, a.t0 + s + 1, ag)
-                           : load_action_w(a, ((long long)(s + 1) * Elong + env) * N + ag);
-    }
-    // ---------------- move decision on the PRE-step map ----------------
-    oc = (r + g.P) * g.pitch + c + g.pl;
-    int nc = oc, pre = 0, av = act;
-    bool moved = false, envc = false;
-    const bool bad_l = has && a.do_step && (act < 0 || act > 4);
-    if (bad_l) av = 4;
-    if (has && a.do_step && !dn && av != 4) {  // __agent_step :319-342
-      const int cand = oc + (av == 0 ? -g.pitch : (av == 1 ? g.pitch : (av == 2 ? -1 : 1)));
-      const uint32_t v = map[cand];
-      if (v == 0x80u) {
-        envc = true;
-      } else {
-        nc = cand;
-        moved = true;
-        pre = (int)(v & 0x7Fu);
+    const uint32_t so = ROLL ? (uint32_t)s * EN : 0u;            // step slot (agents)
+    const uint32_t se = ROLL ? (uint32_t)s * (uint32_t)g.E : 0u;  // step slot (envs)
+    if ((s & (AB - 1)) == 0) {  // actions of steps s .. s+AB-1, packed 4 per u32
+      int v[AB];
+      if (!do_step) {  // observation pass: there is no action buffer
+#pragma unroll
+        for (int k = 0; k < AB; ++k) v[k] = 4;
+      } else if (a.use_rng) {
+#pragma unroll
+        for (int k = 0; k < AB; ++k) v[k] = gen_action(a.seed, g.env_offset + env, a.t0 + s + k, ag);
+      } else if (!ROLL || a.act_dtype != MAPFX_I8) {
+#pragma unroll
+        for (int k = 0; k < AB; ++k)
+          v[k] = (has && s + k < T) ? load_action(a.actions, a.act_dtype, (uint32_t)(s + k) * EN + oa)
+                                    : 4;
+      } else {  // int8 buffer: AB unconditional loads (clamped addresses), one wait
+        const int8_t* ap = (const int8_t*)a.actions;
+        const uint32_t oc_ = has ? oa : 0u;
+#pragma unroll
+        for (int k = 0; k < AB; ++k) v[k] = ap[(uint32_t)min(s + k, T - 1) * EN + oc_];
+      }
+#pragma unroll
+      for (int k = 0; k < (AB + 3) / 4; ++k) actpk[k] = 0;
+#pragma unroll
+      for (int k = 0; k < AB; ++k) {
+        uint32_t u = (uint32_t)v[k];
+        if (!(has && do_step && s + k < T)) u = 4u;
+        if (u > 4u) u = 0xFFu;  // invalid action (the reference asserts, :92)
+        actpk[k >> 2] |= u << (8 * (k & 3));
       }
     }
-    const bool skip = !a.do_step || ((__ballot(bad_l) & envmask) != 0);
-    if (skip) {
-      nc = oc;
-      moved = envc = false;
-    }
+    int act = (int)(actpk[0] & 0xFFu);
+#pragma unroll
+    for (int k = 0; k < (AB + 3) / 4; ++k)  // shift the packed actions down one byte
+      actpk[k] = (k + 1 < (AB + 3) / 4) ? __builtin_amdgcn_alignbit(actpk[k + 1], actpk[k], 8)
+                                        : (actpk[k] >> 8);
+    // ---------------- move decision on the PRE-step map (:319-342) ----------------
+    const int oc = (r + g.P) * pitch + c + g.pl;
+    const bool bad_l = act == 0xFF;
+    const bool mv = !dn && !bad_l && act != 4;  // (has && do_step folded into act == 4)
+    const int cand = oc + (act == 0 ? -pitch : (act == 1 ? pitch : (act == 2 ? -1 : 1)));
+    const uint32_t v = mv ? (uint32_t)map[cand] : 0x80u;
+    const bool envc = mv && v == 0x80u;  // out of bounds / free-standing obstacle (quirk 1)
+    bool moved = mv && v != 0x80u;
+    const int pre = (int)(v & 0x7Fu);
+    const bool skip = !do_step || ((__ballot(bad_l) & envmask) != 0);
+    if (skip) moved = false;
+    const int nc = moved ? cand : oc;
     if (moved) {
       atomicSub(&map32[oc >> 2], 1u << ((oc & 3) * 8));
       atomicAdd(&map32[nc >> 2], 1u << ((nc & 3) * 8));
-      r += act_dr(av);
-      c += act_dc(av);
+      r += act_dr(act);
+      c += act_dc(act);
     }
-    wave_fence();
-    // ---------------- collisions + reward ----------------
-    int node = 0, edge = 0;
-    if (a.do_step && !skip) {
-      node = ((uint32_t)map[nc] & 0x7Fu) > 1u ? 1 : 0;  // :344-362
-    }
-    const bool suspect = moved && pre > 0;  // edge needs j with old_j == new_i (:364-383)
+    // ---------------- edge collisions (:364-383) ----------------
+    int edge = 0;
+    const bool suspect = moved && pre > 0;  // needs j with old_j == new_i
     if (__ballot(suspect)) {
-      // pre == 1: the unique pre-step occupant is who[new cell]
-      const int jw = suspect ? (int)who[r * g.W + c] : 0;
+      const int jw = suspect ? (int)who[r * Wd + c] : 0;  // unique occupant when pre == 1
       const int oj = __shfl(oc, base + jw);
       const int nj = __shfl(nc, base + jw);
       if (suspect && pre == 1) edge = (nj == oc && oj == nc) ? 1 : 0;
@@ -708,8 +749,41 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
         }
       }
     }
-    if (has && a.do_step && !skip) {
-      double rr = 0.0;  // :94-130, exact fp64 op order
+    // ---------------- POST-step map rows: window, node, avail ----------------
+    uint32_t node = 0, availm = 16u;
+    uint32_t o0[WIN > 0 ? WIN : 1], o1[WIN > 0 ? WIN : 1], g0[WIN > 0 ? WIN : 1],
+        g1[WIN > 0 ? WIN : 1];
+    if constexpr (WIN > 0) {
+#pragma unroll
+      for (int y = 0; y < WIN; ++y) {
+        const int a0 = nc + (y - H2) * pitch - H2;  // first cell of the row
+        const int wb = a0 >> 2, o = a0 & 3;
+        const uint32_t lo = map32[wb], hi = map32[wb + 1];
+        const uint32_t hi2 = WIN > 5 ? map32[wb + 2] : 0u;
+        const uint32_t x0 = __builtin_amdgcn_alignbyte(hi, lo, o);
+        const uint32_t x1 = __builtin_amdgcn_alignbyte(hi2, hi, o);
+        swar_window(x0, o0[y], g0[y]);
+        o1[y] = g1[y] = 0;
+        if (WIN > 4) swar_window(x1, o1[y], g1[y]);
+        if (y == H2) {
+          node = (((H2 < 4 ? x0 >> (8 * H2) : x1 >> (8 * (H2 - 4)))) & 0x7Fu) > 1u ? 1u : 0u;
+          availm |= rec_byte<WIN>(y * WIN + H2 - 1, o0, o1, g0, g1) ? 0u : 4u;  // col-1
+          availm |= rec_byte<WIN>(y * WIN + H2 + 1, o0, o1, g0, g1) ? 0u : 8u;  // col+1
+        }
+        if (y == H2 - 1) availm |= rec_byte<WIN>(y * WIN + H2, o0, o1, g0, g1) ? 0u : 1u;
+        if (y == H2 + 1) availm |= rec_byte<WIN>(y * WIN + H2, o0, o1, g0, g1) ? 0u : 2u;
+      }
+    } else {
+      node = ((uint32_t)map[nc] & 0x7Fu) > 1u ? 1u : 0u;
+      availm |= (map[nc - pitch] != 0x80u) ? 1u : 0u;
+      availm |= (map[nc + pitch] != 0x80u) ? 2u : 0u;
+      availm |= (map[nc - 1] != 0x80u) ? 4u : 0u;
+      availm |= (map[nc + 1] != 0x80u) ? 8u : 0u;
+    }
+    if (skip) node = 0;
+    // ---------------- reward (:94-130, exact fp64 op order) and dones ----------------
+    double rr = 0.0;
+    if (!skip) {
       if (!dn) {
         if (envc) rr = rr + g.collide_rew;
         rr = rr + g.step_rew;
@@ -717,146 +791,122 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
       }
       rr = rr + g.collide_rew * (double)node;
       rr = rr + g.collide_rew * (double)edge;
-      rew[ag] = rr;
       if (r == gr && c == gc) dn = true;   // :112-114
-      if (tcur + 1 >= g.limit) dn = true;  // :116-117 (t already incremented below)
-    } else if (has && a.do_step) {
-      rew[ag] = 0.0;
+      if (tcur + 1 >= g.limit) dn = true;  // :116-117 (t is incremented below)
     }
-    if (a.do_step && !skip) ++tcur;
-    // who map for the next step (post-step positions); after every read above
-    if (has) who[r * g.W + c] = (unsigned char)ag;
+    if (has && do_step) rew[ag] = rr;
+    if (!skip) ++tcur;
+    if (has) who[r * Wd + c] = (unsigned char)ag;  // post-step occupant for the next step
     const bool alldone = (__ballot(has && !dn) & envmask) == 0;
+    if constexpr (WIN > 0) {
+      if ((RUNNER || a.obs_window) && has) {  // stage the record as u16 (2-aligned)
+        // volatile LDS (address space 3) u16 stores: keeps them ds_write_b16 instead of
+        // merged, misaligned ds_write_b128s (replayed) or generic flat stores
+        typedef __attribute__((address_space(3))) volatile uint16_t lds_u16;
+        lds_u16* dst = (lds_u16*)(stage + (uint32_t)(slot * N + ag) * REC);
+#pragma unroll
+        for (int k = 0; k < REC / 2; ++k)
+          dst[k] = (uint16_t)(rec_byte<WIN>(2 * k, o0, o1, g0, g1) |
+                              (rec_byte<WIN>(2 * k + 1, o0, o1, g0, g1) << 8));
+      }
+    }
     // ---------------- per-agent outputs ----------------
     if (has) {
-      const long long ai = (slotE + env) * N + ag;
-      if (a.do_step) {
-        if (a.node) a.node[ai] = (uint8_t)node;
-        if (a.edge) a.edge[ai] = (uint8_t)(edge > 255 ? 255 : edge);
-      }
-      if (a.traj_pos) ((int2*)a.traj_pos)[ai] = make_int2(r, c);
-      if (a.traj_done) a.traj_done[ai] = dn ? 1 : 0;
-      if (a.avail) {  // :203-224 on the post-step map
-        uint32_t m = 16u;
-        m |= (map[nc - g.pitch] != 0x80u) ? 1u : 0u;
-        m |= (map[nc + g.pitch] != 0x80u) ? 2u : 0u;
-        m |= (map[nc - 1] != 0x80u) ? 4u : 0u;
-        m |= (map[nc + 1] != 0x80u) ? 8u : 0u;
-        a.avail[ai] = (uint8_t)m;
+      const uint32_t ai = so + oa;
+      if (RUNNER) {
+        a.node[ai] = (uint8_t)node;
+        a.edge[ai] = (uint8_t)(edge > 255 ? 255 : edge);
+        ((int2*)a.traj_pos)[ai] = make_int2(r, c);
+        a.traj_done[ai] = dn ? 1 : 0;
+        a.avail[ai] = (uint8_t)availm;
+      } else {
+        if (do_step) {
+          if (a.node) a.node[ai] = (uint8_t)node;
+          if (a.edge) a.edge[ai] = (uint8_t)(edge > 255 ? 255 : edge);
+        }
+        if (a.traj_pos) ((int2*)a.traj_pos)[ai] = make_int2(r, c);
+        if (a.traj_done) a.traj_done[ai] = dn ? 1 : 0;
+        if (a.avail) a.avail[ai] = (uint8_t)availm;
       }
     }
-    if (WIN > 0 && a.obs_window) {  // marl_partial.py:323-342 via SWAR, staged as u16
-      if (has) {
-        constexpr int WW = WIN * WIN;
-        constexpr int H2 = WIN / 2;
-        // bytes of the agent's record: [obstacle WxW][agents WxW], 2*WW bytes
-        uint32_t ob[(WW + 3) / 4 + 1], agb[(WW + 3) / 4 + 1];
-#pragma unroll
-        for (int k = 0; k < (WW + 3) / 4 + 1; ++k) ob[k] = agb[k] = 0;
-#pragma unroll
-        for (int y = 0; y < WIN; ++y) {
-          const int a0 = nc + (y - H2) * g.pitch - H2;  // first cell of the row
-          const int wb = a0 >> 2, o = a0 & 3;
-          const uint32_t lo = map32[wb], hi = map32[wb + 1];
-          uint32_t hi2 = 0;
-          if (WIN > 5) hi2 = map32[wb + 2];
-          // cells a0 .. a0+WIN-1 as bytes
-          const uint32_t x0 = __builtin_amdgcn_alignbyte(hi, lo, o);
-          const uint32_t x1 = __builtin_amdgcn_alignbyte(hi2, hi, o);
-          uint32_t o0, g0, o1, g1;
-          swar_window(x0, o0, g0);
-          swar_window(x1, o1, g1);
-          // append WIN bytes at byte offset y*WIN of each plane
-#pragma unroll
-          for (int x = 0; x < WIN; ++x) {
-            const uint32_t bo = x < 4 ? (o0 >> (8 * x)) & 0xFFu : (o1 >> (8 * (x - 4))) & 0xFFu;
-            const uint32_t bg = x < 4 ? (g0 >> (8 * x)) & 0xFFu : (g1 >> (8 * (x - 4))) & 0xFFu;
-            const int q = y * WIN + x;  // compile-time
-            ob[q >> 2] |= bo << (8 * (q & 3));
-            agb[q >> 2] |= bg << (8 * (q & 3));
-          }
-        }
-        // record bytes: b[k] = k < WW ? ob-byte k : agb-byte (k - WW); written as u16
-        unsigned char* dst = stage + (size_t)(slot * N + ag) * 2 * WW;
-#pragma unroll
-        for (int k = 0; k < WW; ++k) {
-          const int k0 = 2 * k, k1 = 2 * k + 1;
-          const uint32_t b0 = k0 < WW ? (ob[k0 >> 2] >> (8 * (k0 & 3))) & 0xFFu
-                                      : (agb[(k0 - WW) >> 2] >> (8 * ((k0 - WW) & 3))) & 0xFFu;
-          const uint32_t b1 = k1 < WW ? (ob[k1 >> 2] >> (8 * (k1 & 3))) & 0xFFu
-                                      : (agb[(k1 - WW) >> 2] >> (8 * ((k1 - WW) & 3))) & 0xFFu;
-          *(uint16_t*)(dst + k0) = (uint16_t)(b0 | (b1 << 8));
-        }
-      }
-    }
-    if (a.obs_full && env_ok) {  // :143-192, row-major occ = count - flag
-      unsigned char* outb = (unsigned char*)a.obs_full + (slotE + env) * (long long)g.H * g.W;
-      if ((g.W & 3) == 0) {
-        const int wpr_out = g.W >> 2;
+    if (!RUNNER && a.obs_full && env_ok) {  // :143-192, row-major occ = count - flag
+      unsigned char* outb = (unsigned char*)a.obs_full + (size_t)(se + env) * g.H * Wd;
+      if ((Wd & 3) == 0) {
+        const int wpr_out = Wd >> 2;
         const int nwords = g.H * wpr_out;
         for (int i = ag; i < nwords; i += g.L) {
           const int rr_ = fastdiv(i, g.m_W4);
           const int cw = i - rr_ * wpr_out;
-          const uint32_t v = map32[((rr_ + g.P) * g.pitch + g.pl) / 4 + cw];
-          const uint32_t f = (v >> 7) & 0x01010101u;
-          ((uint32_t*)outb)[i] = (((v & 0x7F7F7F7Fu) | 0x80808080u) - f) ^ 0x80808080u;
+          const uint32_t vv = map32[((rr_ + g.P) * pitch + g.pl) / 4 + cw];
+          const uint32_t f = (vv >> 7) & 0x01010101u;
+          ((uint32_t*)outb)[i] = (((vv & 0x7F7F7F7Fu) | 0x80808080u) - f) ^ 0x80808080u;
         }
       } else {
-        for (int i = ag; i < g.H * g.W; i += g.L) {
+        for (int i = ag; i < g.H * Wd; i += g.L) {
           const int rr_ = fastdiv(i, g.m_W);
-          const int cc_ = i - rr_ * g.W;
-          const uint32_t v = map[(rr_ + g.P) * g.pitch + cc_ + g.pl];
-          ((int8_t*)outb)[i] = (int8_t)((int)(v & 0x7Fu) - (int)(v >> 7));
+          const int cc_ = i - rr_ * Wd;
+          const uint32_t vv = map[(rr_ + g.P) * pitch + cc_ + g.pl];
+          ((int8_t*)outb)[i] = (int8_t)((int)(vv & 0x7Fu) - (int)(vv >> 7));
         }
       }
     }
     wave_fence();
     // ---------------- env outputs: fp64 fold in agent order (:141) ----------------
     if (env_ok && ag == 0) {
-      if (a.do_step) {
+      const uint32_t ei = se + env;
+      if (RUNNER) {
         double R = 0.0;
         for (int j = 0; j < N; ++j) R = R + rew[j];
-        if (a.reward) a.reward[slotE + env] = R;
-        if (a.reward_f32) a.reward_f32[slotE + env] = (float)R;
+        a.reward[ei] = R;
+        if (a.reward_f32) a.reward_f32[ei] = (float)R;
         if (a.err && skip) atomicCAS(a.err, 0, env + 1);
+        a.term[ei] = alldone ? 1 : 0;
+        a.traj_t[ei] = tcur;
+      } else {
+        if (do_step) {
+          double R = 0.0;
+          for (int j = 0; j < N; ++j) R = R + rew[j];
+          if (a.reward) a.reward[ei] = R;
+          if (a.reward_f32) a.reward_f32[ei] = (float)R;
+          if (a.err && skip) atomicCAS(a.err, 0, env + 1);
+        }
+        if (a.term) a.term[ei] = alldone ? 1 : 0;
+        if (a.traj_t) a.traj_t[ei] = tcur;
       }
-      if (a.term) a.term[slotE + env] = alldone ? 1 : 0;
-      if (a.traj_t) a.traj_t[slotE + env] = tcur;
     }
-    if (WIN > 0 && a.obs_window) {  // staging -> HBM, 16 B per lane
-      const int nenv = min(g.EPW, g.E - env0);
-      const long long bytes = (long long)nenv * N * 2 * WIN * WIN;
-      unsigned char* dst =
-          (unsigned char*)a.obs_window + (slotE + env0) * (long long)N * 2 * WIN * WIN;
+    if (WIN > 0 && (RUNNER || a.obs_window)) {  // staging -> HBM, 16 B per lane
+      const int nenv = FULLW ? g.EPW : min(g.EPW, g.E - env0);
+      const uint32_t bytes = (uint32_t)(nenv * N * REC);
+      unsigned char* dst = (unsigned char*)a.obs_window + (size_t)(se + env0) * N * REC;
       if ((((uintptr_t)dst) & 15) == 0 && (bytes & 15) == 0) {
-        for (long long i = lane64; i < (bytes >> 4); i += 64)
+        for (uint32_t i = lane64; i < (bytes >> 4); i += 64)
           ((uint4*)dst)[i] = ((const uint4*)stage)[i];
       } else {
-        for (long long i = lane64; i < bytes; i += 64) dst[i] = stage[i];
+        for (uint32_t i = lane64; i < bytes; i += 64) dst[i] = stage[i];
       }
     }
-    if (ROLL && a.autoreset && a.do_step && alldone && has) {
-      const int2 p = ((const int2*)a.init_pos)[ia];
-      const int ocell = (r + g.P) * g.pitch + c + g.pl;
-      const int ncell = (p.x + g.P) * g.pitch + p.y + g.pl;
-      atomicSub(&map32[ocell >> 2], 1u << ((ocell & 3) * 8));
-      atomicAdd(&map32[ncell >> 2], 1u << ((ncell & 3) * 8));
-      r = p.x;
-      c = p.y;
-      dn = false;
-      st = 0;
-    }
-    if (ROLL && a.autoreset && a.do_step && alldone) {
+    if (ROLL && a.autoreset && alldone) {
+      if (has) {
+        const int2 p = ((const int2*)a.init_pos)[oa];
+        const int ocell = (r + g.P) * pitch + c + g.pl;
+        const int ncell = (p.x + g.P) * pitch + p.y + g.pl;
+        atomicSub(&map32[ocell >> 2], 1u << ((ocell & 3) * 8));
+        atomicAdd(&map32[ncell >> 2], 1u << ((ncell & 3) * 8));
+        r = p.x;
+        c = p.y;
+        dn = false;
+        st = 0;
+      }
       tcur = 0;
       wave_fence();
-      if (has) who[r * g.W + c] = (unsigned char)ag;
+      if (has) who[r * Wd + c] = (unsigned char)ag;
     }
     wave_fence();
   }
   if (has) {
-    ((int2*)a.pos)[ia] = make_int2(r, c);
-    a.done[ia] = dn ? 1 : 0;
-    if (a.steps) a.steps[ia] = st;
+    ((int2*)a.pos)[oa] = make_int2(r, c);
+    a.done[oa] = dn ? 1 : 0;
+    if (a.steps) a.steps[oa] = st;
   }
   if (env_ok && ag == 0) a.t[env] = tcur;
 }
@@ -943,21 +993,21 @@ int check_hip(hipError_t e, const char* what) {
   return MAPFX_OK;
 }
 
-KernelFn pick_wave_kernel(int win, bool roll) {
+template <int WIN>
+KernelFn pick_wave_win(bool roll, bool fullw, bool runner) {
   if (roll) {
-    switch (win) {
-      case 0: return mapf_wave_kernel<0, true>;
-      case 3: return mapf_wave_kernel<3, true>;
-      case 5: return mapf_wave_kernel<5, true>;
-      case 7: return mapf_wave_kernel<7, true>;
-    }
-  } else {
-    switch (win) {
-      case 0: return mapf_wave_kernel<0, false>;
-      case 3: return mapf_wave_kernel<3, false>;
-      case 5: return mapf_wave_kernel<5, false>;
-      case 7: return mapf_wave_kernel<7, false>;
-    }
+    if (runner) return fullw ? mapf_wave_kernel<WIN, true, true, true> : mapf_wave_kernel<WIN, true, false, true>;
+    return fullw ? mapf_wave_kernel<WIN, true, true, false> : mapf_wave_kernel<WIN, true, false, false>;
+  }
+  return fullw ? mapf_wave_kernel<WIN, false, true, false> : mapf_wave_kernel<WIN, false, false, false>;
+}
+
+KernelFn pick_wave_kernel(int win, bool roll, bool fullw, bool runner) {
+  switch (win) {
+    case 0: return pick_wave_win<0>(roll, fullw, runner);
+    case 3: return pick_wave_win<3>(roll, fullw, runner);
+    case 5: return pick_wave_win<5>(roll, fullw, runner);
+    case 7: return pick_wave_win<7>(roll, fullw, runner);
   }
   return nullptr;
 }
@@ -966,8 +1016,14 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream) {
   const Geo& g = h->geo;
   if (g.E == 0) return MAPFX_OK;
   // wave-local fast path: N <= 64, no PRIMAL output, window 3/5/7 (or none)
-  if (g.wave_ok && !a.obs_primal && !a.primal_vec) {
-    KernelFn fn = pick_wave_kernel(a.obs_window ? g.window : 0, roll);
+  const long long slot_elems = (long long)(roll ? a.T : 1) * g.E * g.N;
+  const bool fits32 = slot_elems * std::max(8, 2 * g.window * g.window) < (1ll << 31) &&
+                      (long long)(roll ? a.T : 1) * g.E * g.H * g.W < (1ll << 31);
+  if (g.wave_ok && fits32 && !a.obs_primal && !a.primal_vec) {
+    const bool fullw = g.N == g.L && g.E % g.EPW == 0;
+    const bool runner = roll && a.reward && a.term && a.node && a.edge && a.avail &&
+                        a.traj_pos && a.traj_done && a.traj_t && a.obs_window && !a.obs_full;
+    KernelFn fn = pick_wave_kernel(a.obs_window ? g.window : 0, roll, fullw, runner);
     if (fn) {
       const int blocks = (g.E + g.EPW - 1) / g.EPW;
       hipLaunchKernelGGL(fn, dim3(blocks), dim3(64), g.wv_lds, stream, g, a);

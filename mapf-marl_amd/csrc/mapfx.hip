@@ -32,6 +32,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <utility>
 #include <new>
 #include <string>
 
@@ -94,8 +95,8 @@ struct Geo {
   double step_rew, collide_rew;
   // wave-local fast path (N <= 64: an env never spans two wavefronts)
   int wave_ok, EPW;
-  int wv_off_map, wv_off_who, wv_off_bits, wv_off_rew, wv_off_stage, wv_lds;
-  int who_env_bytes, wv_bits_env_bytes;
+  int wv_off_map, wv_off_dep, wv_off_bits, wv_off_rew, wv_off_stage, wv_lds;
+  int wv_bits_env_bytes, wv_rew_buf, wv_stage_buf, wv_rew_row;  // rew / staging are double-buffered
 };
 
 struct Args {
@@ -561,6 +562,30 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
 //   agent order; the wave writes the staged records with 16-byte stores.
 // Actions for step s+1 are loaded while step s runs.  All offsets are 32-bit.
 // ===========================================================================
+#ifndef MAPFX_DIRECT_REC
+#define MAPFX_DIRECT_REC 1
+#endif
+#ifndef MAPFX_ABLATE
+#define MAPFX_ABLATE 0  // diagnostic builds only: bit mask of parts skipped for timing
+#endif
+#ifdef MAPFX_STAMPS
+// Diagnostic build only (never the shipped library): per-segment s_memtime stamps
+// of block 0 / lane 0, read back with mapfx_debug_stamps().
+__device__ unsigned long long g_stamps[256 * 8];
+#define STAMP(k)                                                                  \
+  do {                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    unsigned long long t_;                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && s < 256) g_stamps[s * 8 + (k)] = t_; \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
 __device__ inline void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -586,20 +611,119 @@ __device__ __forceinline__ void put_bits(uint64_t (&w)[NW], int pos, int bits, u
   if (sh + bits > 64 && wi + 1 < NW) w[wi + 1] |= chunk >> (64 - sh);
 }
 
-// Byte b of the packed window record held in registers: obstacle plane
-// (rows o0[y]: cols 0-3, o1[y]: col 4-7), then agents plane (g0[y], g1[y]).
+// ---- window record packing ------------------------------------------------
+// The record of one agent is 2*WIN*WIN bytes: obstacle plane rows then agents
+// plane rows.  Row y of a plane lives in two registers: cols 0-3 (R[.. + y]) and
+// cols 4-7 (R[.. + WIN + y]).  Register index of record byte b and its byte lane:
 template <int WIN>
-__device__ __forceinline__ uint32_t rec_byte(int b, const uint32_t* o0, const uint32_t* o1,
-                                             const uint32_t* g0, const uint32_t* g1) {
-  constexpr int WW = WIN * WIN;
-  const int pl = b / WW, q = b % WW, y = q / WIN, x = q % WIN;
-  const uint32_t src = pl == 0 ? (x < 4 ? o0[y] : o1[y]) : (x < 4 ? g0[y] : g1[y]);
-  return (src >> (8 * (x & 3))) & 0xFFu;
+__host__ __device__ constexpr int rec_reg(int b) {
+  return (b / (WIN * WIN)) * 2 * WIN + ((b % (WIN * WIN)) % WIN >= 4 ? WIN : 0) +
+         (b % (WIN * WIN)) / WIN;
+}
+template <int WIN>
+__host__ __device__ constexpr int rec_lane(int b) {
+  return ((b % (WIN * WIN)) % WIN) & 3;
+}
+// Dword k of the record (bytes 4k..4k+3) as at most two v_perm_b32 of register pairs.
+struct PermSpec {
+  int ra, rb, rc, rd;  // perm(R[rb], R[ra], s1) | perm(R[rd], R[rc], s2); rc < 0: one perm
+  uint32_t s1, s2;
+};
+template <int WIN>
+__host__ __device__ constexpr PermSpec perm_spec(int k) {
+  constexpr int REC = 2 * WIN * WIN;
+  PermSpec sp{-1, -1, -1, -1, 0x0C0C0C0Cu, 0x0C0C0C0Cu};
+  for (int j = 0; j < 4; ++j) {
+    const int b = 4 * k + j;
+    if (b >= REC) continue;
+    const int r = rec_reg<WIN>(b), l = rec_lane<WIN>(b);
+    const uint32_t clr = ~(0xFFu << (8 * j));
+    if (sp.ra < 0 || sp.ra == r) {
+      sp.ra = r;
+      sp.s1 = (sp.s1 & clr) | ((uint32_t)l << (8 * j));
+    } else if (sp.rb < 0 || sp.rb == r) {
+      sp.rb = r;
+      sp.s1 = (sp.s1 & clr) | ((uint32_t)(4 + l) << (8 * j));
+    } else if (sp.rc < 0 || sp.rc == r) {
+      sp.rc = r;
+      sp.s2 = (sp.s2 & clr) | ((uint32_t)l << (8 * j));
+    } else {
+      sp.rd = r;
+      sp.s2 = (sp.s2 & clr) | ((uint32_t)(4 + l) << (8 * j));
+    }
+  }
+  return sp;
+}
+
+// Record word k (bytes 4k..4k+3) from the row registers (<= 2 v_perm_b32).
+template <int WIN, int K>
+__device__ __forceinline__ uint32_t rec_word(const uint32_t (&R)[4 * WIN]) {
+  constexpr PermSpec sp = perm_spec<WIN>(K);
+  uint32_t w = __builtin_amdgcn_perm(sp.rb >= 0 ? R[sp.rb >= 0 ? sp.rb : 0] : 0u, R[sp.ra], sp.s1);
+  if constexpr (sp.rc >= 0)
+    w |= __builtin_amdgcn_perm(sp.rd >= 0 ? R[sp.rd >= 0 ? sp.rd : 0] : 0u, R[sp.rc], sp.s2);
+  return w;
+}
+
+template <int WIN, int... K>
+__device__ __forceinline__ void rec_words(const uint32_t (&R)[4 * WIN], uint32_t* w,
+                                          std::integer_sequence<int, K...>) {
+  ((w[K] = rec_word<WIN, K>(R)), ...);
+}
+
+// Direct HBM variant of stage_record (diagnostic comparison, MAPFX_DIRECT_REC=1):
+// same split into one u16 + dword stores, written straight to global memory.
+template <int WIN>
+__device__ __forceinline__ void write_record(const uint32_t (&R)[4 * WIN], unsigned char* rec) {
+  constexpr int REC = 2 * WIN * WIN;
+  constexpr int NW = (REC + 3) / 4;
+  constexpr int ND = (REC - 2) / 4;
+  uint32_t w[NW];
+  rec_words<WIN>(R, w, std::make_integer_sequence<int, NW>{});
+  const bool odd = (((uintptr_t)rec) & 2) != 0;
+  unsigned char* dbase = rec + (odd ? 2 : 0);
+#pragma unroll
+  for (int j = 0; j < ND; ++j)
+    *(uint32_t*)(dbase + 4 * j) = odd ? __builtin_amdgcn_alignbyte(w[j + 1], w[j], 2) : w[j];
+  *(uint16_t*)(rec + (odd ? 0 : REC - 2)) = (uint16_t)(odd ? w[0] : w[NW - 1]);
+}
+
+// 32-bit LDS address of a pointer into dynamic shared memory
+__device__ __forceinline__ __attribute__((unused)) uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// Stage one agent's 2*WIN*WIN-byte window record in LDS.  Records are 2-byte
+// aligned (2*WIN^2 = 2 mod 4 for odd WIN): a record at 2 mod 4 is written as one
+// u16 then dwords shifted by two bytes, one at 0 mod 4 as dwords then one u16,
+// so every store is naturally aligned (ds_write_b32 / ds_write2_b32, never the
+// replayed misaligned forms) and no byte of a neighbour's record is touched.
+// The wave then moves its staged block to HBM with coalesced 16-byte stores --
+// 13x faster than the same bytes as scattered per-lane dword stores
+// (tools/micro/stores.hip: 0.51 vs 6.4 us per 3.2 MB on MI355X).
+template <int WIN>
+__device__ __forceinline__ void stage_record(const uint32_t (&R)[4 * WIN], unsigned char* rec) {
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  typedef __attribute__((address_space(3))) uint16_t lds_u16;
+  constexpr int REC = 2 * WIN * WIN;
+  constexpr int NW = (REC + 3) / 4;
+  constexpr int ND = (REC - 2) / 4;
+  static_assert(REC % 4 == 2, "odd window sizes only");
+  uint32_t w[NW];
+  rec_words<WIN>(R, w, std::make_integer_sequence<int, NW>{});
+  const uint32_t ra = lds_addr(rec);
+  const bool odd = (ra & 2) != 0;
+  lds_u32* d = (lds_u32*)(uintptr_t)(ra + (odd ? 2 : 0));
+#pragma unroll
+  for (int j = 0; j < ND; ++j) d[j] = odd ? __builtin_amdgcn_alignbyte(w[j + 1], w[j], 2) : w[j];
+  *(lds_u16*)(uintptr_t)(ra + (odd ? 0 : REC - 2)) = (uint16_t)(odd ? w[0] : w[NW - 1]);
 }
 
 // FULLW: every lane owns an agent (N == L and E % EPW == 0) -> no lane masks.
 // RUNNER (rollout only): the standard runner outputs are all present (reward,
 // term, node, edge, avail, traj_pos/done/t, window obs) -> no per-output tests.
+// Rollouts software-pipeline each step's tail (fp64 fold, env outputs, window
+// copy-out; double-buffered rew/staging) into the next step's LDS latencies.
 template <int WIN, bool ROLL, bool FULLW, bool RUNNER>
 __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   extern __shared__ __align__(16) unsigned char lds[];
@@ -619,13 +743,13 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   const uint64_t envmask = (g.L == 64 ? ~0ull : ((1ull << g.L) - 1ull)) << base;
   const int pitch = g.pitch;
   const int Wd = g.W;
+  const bool want_win = WIN > 0 && (RUNNER || a.obs_window);
+  const int nenv = FULLW ? g.EPW : min(g.EPW, g.E - env0);
 
   unsigned char* map = lds + g.wv_off_map + slot * g.map_env_bytes;
   uint32_t* map32 = (uint32_t*)map;
-  unsigned char* who = lds + g.wv_off_who + slot * g.who_env_bytes;
+  unsigned char* dep = lds + g.wv_off_dep + slot * g.map_env_bytes;  // move dir per old cell
   uint32_t* bitsL = (uint32_t*)(lds + g.wv_off_bits + slot * g.wv_bits_env_bytes);
-  double* rew = (double*)(lds + g.wv_off_rew) + slot * N;
-  unsigned char* stage = lds + g.wv_off_stage;  // [EPW][N][REC]
 
   const uint32_t oa = (uint32_t)(env * N + ag);  // agent index inside one step slot
   const uint32_t EN = (uint32_t)(g.E * N);
@@ -648,7 +772,7 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   constexpr int AB = ROLL ? 16 : 1;
   uint32_t actpk[(AB + 3) / 4];
 
-  // ---- bitmap -> LDS, padded map, agents, who map ----
+  // ---- bitmap -> LDS, padded map, agents ----
   if (env_ok) {
     const uint32_t* src =
         (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)env * g.map_stride));
@@ -674,13 +798,79 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   if (has) {
     const int oc = (r + g.P) * pitch + c + g.pl;
     atomicAdd(&map32[oc >> 2], 1u << ((oc & 3) * 8));
-    who[r * Wd + c] = (unsigned char)ag;
   }
   wave_fence();
 
+  // tail of step s (fold, env outputs, window copy-out) — runs one step late in rollouts
+  // rewards of a step are folded from LDS (rew[buf]: one row of N fp64 per env,
+  // padded with +0.0 to a multiple of 2; adding +0.0 never changes a sum that
+  // starts at +0.0) -- as 16 independent-of-this-step adds the scheduler can
+  // interleave with the window work.
+  const int rew_row = g.wv_rew_row;  // doubles per env row
+  auto fold = [&](int buf) {
+    const double* rw = (const double*)(lds + g.wv_off_rew + buf * g.wv_rew_buf) + slot * rew_row;
+    double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
+    if (MAPFX_ABLATE & 2) return R;
+    if (g.L == 16) {  // all 16 lanes wrote their slot (+0.0 past N)
+      double v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = rw[j];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) R = R + v[j];
+    } else {
+      for (int j = 0; j < N; ++j) R = R + rw[j];
+    }
+    return R;
+  };
+  // tail of step s (env outputs, window copy-out) -- runs one step late in rollouts
+  auto tail = [&](int buf, uint32_t se_t, bool skip_t, bool alldone_t, int tcur_t, double R) {
+    if (env_ok && ag == 0) {
+      const uint32_t ei = se_t + env;
+      if (RUNNER) {
+        a.reward[ei] = R;
+        a.term[ei] = alldone_t ? 1 : 0;
+        a.traj_t[ei] = tcur_t;
+      } else {
+        if (do_step && a.reward) a.reward[ei] = R;
+        if (a.term) a.term[ei] = alldone_t ? 1 : 0;
+        if (a.traj_t) a.traj_t[ei] = tcur_t;
+      }
+      if (do_step && a.reward_f32) a.reward_f32[ei] = (float)R;
+      if (do_step && a.err && skip_t) atomicCAS(a.err, 0, env + 1);
+    }
+    if (want_win && !MAPFX_DIRECT_REC && !(MAPFX_ABLATE & 4)) {  // staging -> HBM, 16 B/lane
+      const unsigned char* stg = lds + g.wv_off_stage + buf * g.wv_stage_buf;
+      const uint32_t bytes = (uint32_t)(nenv * N * REC);
+      unsigned char* dst = (unsigned char*)a.obs_window + (size_t)(se_t + env0) * N * REC;
+      if ((((uintptr_t)dst) & 15) == 0 && (bytes & 15) == 0) {
+        for (uint32_t i = lane64; i < (bytes >> 4); i += 64)
+          ((uint4*)dst)[i] = ((const uint4*)stg)[i];
+      } else {
+        for (uint32_t i = lane64; i < bytes; i += 64) dst[i] = stg[i];
+      }
+    }
+  };
+
+  uint32_t p_se = 0;
+  bool p_skip = false, p_alldone = false;
+  int p_tcur = 0;
+  // Retire the state loads here (s_waitcnt vmcnt(0), gfx9 encoding): otherwise the
+  // waitcnt pass merges "load pending" into the loop header and re-waits vmcnt(0)
+  // -- i.e. drains every outstanding store -- at each use of r/c/t inside the loop.
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  // Raw map bytes of the 4 neighbours (byte d = cell of action d), carried from the
+  // end of one step (post-step map) to the move decision of the next (pre-step
+  // map): the move test needs no LDS round trip.
+  uint32_t nb = 0;
+  if (has) {
+    const int oc = (r + g.P) * pitch + c + g.pl;
+    nb = (uint32_t)map[oc - pitch] | ((uint32_t)map[oc + pitch] << 8) |
+         ((uint32_t)map[oc - 1] << 16) | ((uint32_t)map[oc + 1] << 24);
+  }
   for (int s = 0; s < T; ++s) {
     const uint32_t so = ROLL ? (uint32_t)s * EN : 0u;            // step slot (agents)
     const uint32_t se = ROLL ? (uint32_t)s * (uint32_t)g.E : 0u;  // step slot (envs)
+    const int buf = ROLL ? (s & 1) : 0;
     if ((s & (AB - 1)) == 0) {  // actions of steps s .. s+AB-1, packed 4 per u32
       int v[AB];
       if (!do_step) {  // observation pass: there is no action buffer
@@ -710,37 +900,66 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
         actpk[k >> 2] |= u << (8 * (k & 3));
       }
     }
-    int act = (int)(actpk[0] & 0xFFu);
+    const int act = (int)(actpk[0] & 0xFFu);
 #pragma unroll
     for (int k = 0; k < (AB + 3) / 4; ++k)  // shift the packed actions down one byte
       actpk[k] = (k + 1 < (AB + 3) / 4) ? __builtin_amdgcn_alignbit(actpk[k + 1], actpk[k], 8)
                                         : (actpk[k] >> 8);
+    STAMP(0);
     // ---------------- move decision on the PRE-step map (:319-342) ----------------
     const int oc = (r + g.P) * pitch + c + g.pl;
     const bool bad_l = act == 0xFF;
-    const bool mv = !dn && !bad_l && act != 4;  // (has && do_step folded into act == 4)
+    const bool mv = !dn && !bad_l && act != 4;  // (!has / observe lanes carry act == 4)
     const int cand = oc + (act == 0 ? -pitch : (act == 1 ? pitch : (act == 2 ? -1 : 1)));
-    const uint32_t v = mv ? (uint32_t)map[cand] : 0x80u;
+    const uint32_t v = mv ? ((nb >> (8 * (act & 3))) & 0xFFu) : 0x80u;  // pre-step cell
+    STAMP(7);
+    STAMP(1);
     const bool envc = mv && v == 0x80u;  // out of bounds / free-standing obstacle (quirk 1)
-    bool moved = mv && v != 0x80u;
-    const int pre = (int)(v & 0x7Fu);
     const bool skip = !do_step || ((__ballot(bad_l) & envmask) != 0);
-    if (skip) moved = false;
+    const bool moved = mv && v != 0x80u && !skip;
+    const int pre = (int)(v & 0x7Fu);
     const int nc = moved ? cand : oc;
+    if (has && !(MAPFX_ABLATE & 64)) dep[oc] = moved ? (unsigned char)act : (unsigned char)0xFF;
     if (moved) {
-      atomicSub(&map32[oc >> 2], 1u << ((oc & 3) * 8));
-      atomicAdd(&map32[nc >> 2], 1u << ((nc & 3) * 8));
+      if (!(MAPFX_ABLATE & 16)) {
+        atomicSub(&map32[oc >> 2], 1u << ((oc & 3) * 8));
+        atomicAdd(&map32[nc >> 2], 1u << ((nc & 3) * 8));
+      }
       r += act_dr(act);
       c += act_dc(act);
     }
+    STAMP(2);
     // ---------------- edge collisions (:364-383) ----------------
+    // i moved into a cell X that had pre-step occupants; j counts iff j moved from
+    // X back into i's old cell, i.e. in the opposite direction (act ^ 1).
+    // POST-step rows of the window (or the 4 neighbours), the occupant's move, and
+    // the previous step's tail are all issued before any of them is waited for.
+    uint32_t xlo[WIN > 0 ? WIN : 1], xhi[WIN > 0 ? WIN : 1], xhi2[WIN > 0 ? WIN : 1];
+    uint32_t nbw[4];
+    if constexpr (WIN > 0) {
+#pragma unroll
+      for (int y = 0; y < WIN; ++y) {
+        const int wb = (nc + (y - H2) * pitch - H2) >> 2;
+        xlo[y] = map32[wb];
+        xhi[y] = map32[wb + 1];
+        xhi2[y] = WIN > 5 ? map32[wb + 2] : 0u;
+      }
+    } else if (!(MAPFX_ABLATE & 32)) {
+      nbw[0] = map[nc - pitch];
+      nbw[1] = map[nc + pitch];
+      nbw[2] = map[nc - 1];
+      nbw[3] = map[nc + 1];
+      nbw[0] |= (uint32_t)map[nc] << 8;  // centre (node) in byte 1 of nbw[0]
+    } else {
+      nbw[0] = nbw[1] = nbw[2] = nbw[3] = 1u;
+    }
+    const uint32_t dj = (MAPFX_ABLATE & 64) ? 0xFFu : dep[nc];  // pre-step occupant's move
+    const double R_prev = (ROLL && s > 0 && do_step) ? fold(buf ^ 1) : 0.0;
+    if (ROLL && s > 0) tail(buf ^ 1, p_se, p_skip, p_alldone, p_tcur, R_prev);
     int edge = 0;
-    const bool suspect = moved && pre > 0;  // needs j with old_j == new_i
+    const bool suspect = moved && pre > 0;
     if (__ballot(suspect)) {
-      const int jw = suspect ? (int)who[r * Wd + c] : 0;  // unique occupant when pre == 1
-      const int oj = __shfl(oc, base + jw);
-      const int nj = __shfl(nc, base + jw);
-      if (suspect && pre == 1) edge = (nj == oc && oj == nc) ? 1 : 0;
+      if (suspect && pre == 1) edge = dj == (uint32_t)(act ^ 1) ? 1 : 0;
       if (__ballot(suspect && pre > 1)) {  // stacked pre-occupants: scan the env
         for (int j = 0; j < N; ++j) {
           const int oj2 = __shfl(oc, base + j);
@@ -749,41 +968,36 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
         }
       }
     }
+    STAMP(3);
     // ---------------- POST-step map rows: window, node, avail ----------------
     uint32_t node = 0, availm = 16u;
-    uint32_t o0[WIN > 0 ? WIN : 1], o1[WIN > 0 ? WIN : 1], g0[WIN > 0 ? WIN : 1],
-        g1[WIN > 0 ? WIN : 1];
+    uint32_t R[WIN > 0 ? 4 * WIN : 1];  // [plane][cols 0-3 | cols 4-7][row]
     if constexpr (WIN > 0) {
+      uint32_t X0[WIN], X1[WIN];
 #pragma unroll
       for (int y = 0; y < WIN; ++y) {
-        const int a0 = nc + (y - H2) * pitch - H2;  // first cell of the row
-        const int wb = a0 >> 2, o = a0 & 3;
-        const uint32_t lo = map32[wb], hi = map32[wb + 1];
-        const uint32_t hi2 = WIN > 5 ? map32[wb + 2] : 0u;
-        const uint32_t x0 = __builtin_amdgcn_alignbyte(hi, lo, o);
-        const uint32_t x1 = __builtin_amdgcn_alignbyte(hi2, hi, o);
-        swar_window(x0, o0[y], g0[y]);
-        o1[y] = g1[y] = 0;
-        if (WIN > 4) swar_window(x1, o1[y], g1[y]);
-        if (y == H2) {
-          node = (((H2 < 4 ? x0 >> (8 * H2) : x1 >> (8 * (H2 - 4)))) & 0x7Fu) > 1u ? 1u : 0u;
-          availm |= rec_byte<WIN>(y * WIN + H2 - 1, o0, o1, g0, g1) ? 0u : 4u;  // col-1
-          availm |= rec_byte<WIN>(y * WIN + H2 + 1, o0, o1, g0, g1) ? 0u : 8u;  // col+1
-        }
-        if (y == H2 - 1) availm |= rec_byte<WIN>(y * WIN + H2, o0, o1, g0, g1) ? 0u : 1u;
-        if (y == H2 + 1) availm |= rec_byte<WIN>(y * WIN + H2, o0, o1, g0, g1) ? 0u : 2u;
+        const int o = (nc + (y - H2) * pitch - H2) & 3;
+        X0[y] = __builtin_amdgcn_alignbyte(xhi[y], xlo[y], o);   // cells 0-3 of the row
+        X1[y] = __builtin_amdgcn_alignbyte(xhi2[y], xhi[y], o);  // cells 4-7
+        swar_window(X0[y], R[y], R[2 * WIN + y]);
+        R[WIN + y] = R[3 * WIN + y] = 0;
+        if (WIN > 4) swar_window(X1[y], R[WIN + y], R[3 * WIN + y]);
       }
+      const auto raw = [&](int y, int x) { return ((x >= 4 ? X1[y] : X0[y]) >> (8 * (x & 3))) & 0xFFu; };
+      node = (raw(H2, H2) & 0x7Fu) > 1u ? 1u : 0u;
+      nb = raw(H2 - 1, H2) | (raw(H2 + 1, H2) << 8) | (raw(H2, H2 - 1) << 16) | (raw(H2, H2 + 1) << 24);
     } else {
-      node = ((uint32_t)map[nc] & 0x7Fu) > 1u ? 1u : 0u;
-      availm |= (map[nc - pitch] != 0x80u) ? 1u : 0u;
-      availm |= (map[nc + pitch] != 0x80u) ? 2u : 0u;
-      availm |= (map[nc - 1] != 0x80u) ? 4u : 0u;
-      availm |= (map[nc + 1] != 0x80u) ? 8u : 0u;
+      node = ((nbw[0] >> 8) & 0x7Fu) > 1u ? 1u : 0u;
+      nb = (nbw[0] & 0xFFu) | (nbw[1] << 8) | (nbw[2] << 16) | (nbw[3] << 24);
     }
+    // avail (:203-224): a neighbour is available iff it is not (obstacle, 0 agents)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) availm |= (((nb >> (8 * d)) & 0xFFu) != 0x80u) ? (1u << d) : 0u;
     if (skip) node = 0;
+    STAMP(4);
     // ---------------- reward (:94-130, exact fp64 op order) and dones ----------------
     double rr = 0.0;
-    if (!skip) {
+    if (!skip && !(MAPFX_ABLATE & 128)) {
       if (!dn) {
         if (envc) rr = rr + g.collide_rew;
         rr = rr + g.step_rew;
@@ -794,24 +1008,22 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
       if (r == gr && c == gc) dn = true;   // :112-114
       if (tcur + 1 >= g.limit) dn = true;  // :116-117 (t is incremented below)
     }
-    if (has && do_step) rew[ag] = rr;
+    if (do_step && ag < rew_row)  // lanes past N pad the row with +0.0
+      ((double*)(lds + g.wv_off_rew + buf * g.wv_rew_buf))[slot * rew_row + ag] = has ? rr : 0.0;
     if (!skip) ++tcur;
-    if (has) who[r * Wd + c] = (unsigned char)ag;  // post-step occupant for the next step
     const bool alldone = (__ballot(has && !dn) & envmask) == 0;
     if constexpr (WIN > 0) {
-      if ((RUNNER || a.obs_window) && has) {  // stage the record as u16 (2-aligned)
-        // volatile LDS (address space 3) u16 stores: keeps them ds_write_b16 instead of
-        // merged, misaligned ds_write_b128s (replayed) or generic flat stores
-        typedef __attribute__((address_space(3))) volatile uint16_t lds_u16;
-        lds_u16* dst = (lds_u16*)(stage + (uint32_t)(slot * N + ag) * REC);
-#pragma unroll
-        for (int k = 0; k < REC / 2; ++k)
-          dst[k] = (uint16_t)(rec_byte<WIN>(2 * k, o0, o1, g0, g1) |
-                              (rec_byte<WIN>(2 * k + 1, o0, o1, g0, g1) << 8));
+      if (want_win && has && !(MAPFX_ABLATE & 1)) {
+#if MAPFX_DIRECT_REC
+        write_record<WIN>(R, (unsigned char*)a.obs_window + (size_t)(so + oa) * REC);
+#else
+        stage_record<WIN>(R, lds + g.wv_off_stage + buf * g.wv_stage_buf +
+                                 (uint32_t)(slot * N + ag) * REC);  // -> LDS staging
+#endif
       }
     }
     // ---------------- per-agent outputs ----------------
-    if (has) {
+    if (has && !(MAPFX_ABLATE & 8)) {
       const uint32_t ai = so + oa;
       if (RUNNER) {
         a.node[ai] = (uint8_t)node;
@@ -851,39 +1063,14 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
       }
     }
     wave_fence();
-    // ---------------- env outputs: fp64 fold in agent order (:141) ----------------
-    if (env_ok && ag == 0) {
-      const uint32_t ei = se + env;
-      if (RUNNER) {
-        double R = 0.0;
-        for (int j = 0; j < N; ++j) R = R + rew[j];
-        a.reward[ei] = R;
-        if (a.reward_f32) a.reward_f32[ei] = (float)R;
-        if (a.err && skip) atomicCAS(a.err, 0, env + 1);
-        a.term[ei] = alldone ? 1 : 0;
-        a.traj_t[ei] = tcur;
-      } else {
-        if (do_step) {
-          double R = 0.0;
-          for (int j = 0; j < N; ++j) R = R + rew[j];
-          if (a.reward) a.reward[ei] = R;
-          if (a.reward_f32) a.reward_f32[ei] = (float)R;
-          if (a.err && skip) atomicCAS(a.err, 0, env + 1);
-        }
-        if (a.term) a.term[ei] = alldone ? 1 : 0;
-        if (a.traj_t) a.traj_t[ei] = tcur;
-      }
-    }
-    if (WIN > 0 && (RUNNER || a.obs_window)) {  // staging -> HBM, 16 B per lane
-      const int nenv = FULLW ? g.EPW : min(g.EPW, g.E - env0);
-      const uint32_t bytes = (uint32_t)(nenv * N * REC);
-      unsigned char* dst = (unsigned char*)a.obs_window + (size_t)(se + env0) * N * REC;
-      if ((((uintptr_t)dst) & 15) == 0 && (bytes & 15) == 0) {
-        for (uint32_t i = lane64; i < (bytes >> 4); i += 64)
-          ((uint4*)dst)[i] = ((const uint4*)stage)[i];
-      } else {
-        for (uint32_t i = lane64; i < bytes; i += 64) dst[i] = stage[i];
-      }
+    STAMP(6);
+    p_se = se;
+    p_skip = skip;
+    p_alldone = alldone;
+    p_tcur = tcur;
+    if (!ROLL) {
+      wave_fence();
+      tail(buf, se, skip, alldone, tcur, do_step ? fold(buf) : 0.0);
     }
     if (ROLL && a.autoreset && alldone) {
       if (has) {
@@ -899,10 +1086,15 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
       }
       tcur = 0;
       wave_fence();
-      if (has) who[r * Wd + c] = (unsigned char)ag;
+      if (has) {
+        const int o2 = (r + g.P) * pitch + c + g.pl;
+        nb = (uint32_t)map[o2 - pitch] | ((uint32_t)map[o2 + pitch] << 8) |
+             ((uint32_t)map[o2 - 1] << 16) | ((uint32_t)map[o2 + 1] << 24);
+      }
     }
     wave_fence();
   }
+  if (ROLL && T > 0) tail((T - 1) & 1, p_se, p_skip, p_alldone, p_tcur, fold((T - 1) & 1));
   if (has) {
     ((int2*)a.pos)[oa] = make_int2(r, c);
     a.done[oa] = dn ? 1 : 0;
@@ -1091,6 +1283,13 @@ extern "C" {
 
 int mapfx_abi_version(void) { return MAPFX_ABI_VERSION; }
 
+#ifdef MAPFX_STAMPS
+int mapfx_debug_stamps(unsigned long long* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 256 * 8) ==
+                 hipSuccess ? 0 : -1;
+}
+#endif
+
 const char* mapfx_last_error(void) { return g_last_error.c_str(); }
 
 int64_t mapfx_map_stride(int32_t H, int32_t W) {
@@ -1231,19 +1430,23 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   if (L <= 64 && es == 1) {
     const int EPW = 64 / L;
     g.EPW = EPW;
-    g.who_env_bytes = round_up(c.H * c.W, 16);
     g.wv_bits_env_bytes = round_up(g.bits_words * 4 + 4, 16);
     int o = 0;
     g.wv_off_map = o;
     o += EPW * g.map_env_bytes;
-    g.wv_off_who = o;
-    o += EPW * g.who_env_bytes;
+    g.wv_off_dep = o;
+    o += EPW * g.map_env_bytes;
     g.wv_off_bits = o;
     o += EPW * g.wv_bits_env_bytes;
+    // rew rows: N doubles rounded up to 2 (16 B), +2 doubles so the 4 envs of a wave
+    // start on different banks
+    g.wv_rew_row = (N + 1) / 2 * 2 + ((((N + 1) / 2 * 2) % 16) == 0 ? 2 : 0);
+    g.wv_rew_buf = round_up(EPW * g.wv_rew_row * 8, 16);
     g.wv_off_rew = o;
-    o += round_up(EPW * N * 8, 16);
+    o += 2 * g.wv_rew_buf;
+    g.wv_stage_buf = round_up(EPW * g.stage_env_bytes, 16);
     g.wv_off_stage = o;
-    o += EPW * g.stage_env_bytes;
+    o += 2 * g.wv_stage_buf;
     g.wv_lds = o;
     g.wave_ok = (o <= 64 * 1024) ? 1 : 0;
   }

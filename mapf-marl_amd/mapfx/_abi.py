@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must precede loading libmapfx.so: shared HIP runtime)
 
 LIB_NAME = "libmapfx.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_PATH = os.environ.get("MAPFX_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 MAPFX_OBS_FULL = 1
 MAPFX_OBS_WINDOW = 2

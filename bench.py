@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--chunk", type=int, default=64, help="env steps per rollout launch")
     ap.add_argument("--window", type=int, default=5)
     ap.add_argument("--per-step-steps", type=int, default=200)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU work of the cpu_baseline sample (0 disables)")
     ap.add_argument("--gather", action="store_true",
                     help="also time the RCCL gather of (obs, reward, done) to rank 0")
@@ -94,7 +94,7 @@ def main():
     K, WU, T = args.steps, args.warmup, args.chunk
     if K % T or WU % T:
         T = int(np.gcd(K, max(WU, T)) or 1)
-    offset = rank * E
+    offset = rank * E                 # weak scaling: rank r owns global envs [r*E, (r+1)*E)
     inst = synthetic_instances(E, S, S, N, p_obstacle=p or 0.0, seed=1, env_offset=offset,
                                shared_grid=warehouse_grid(S) if shared else None)
     limit = 2 ** 31 - 1
@@ -184,7 +184,7 @@ def main():
     # ---- optional RCCL gather of (obs, reward, done) to rank 0 ----
     gather = None
     if dist and args.gather:
-        gather = time_gather(dist, b, acts, traj, outs, T, WU, K, rank, world, E, N)
+        gather = time_gather(dist, b, acts, outs, T, WU, K, world, E, N)
 
     # ---- CPU baseline: the oracle's C restatement on this host (rank 0, N=1) ----
     cpu = None
@@ -236,43 +236,26 @@ def main():
         dist.destroy_process_group()
 
 
-def time_gather(dist, b, acts, traj, outs, T, WU, K, rank, world, E, N):
-    """Rollout chunks with the chunk's (window obs, reward, done) gathered to rank 0
-    over RCCL on a side stream, overlapped with the next chunk."""
-    side = torch.cuda.Stream()
-    bufs = [b._alloc_out(T), b._alloc_out(T)]
-    for bb in bufs:
-        bb.pop("reward_f32")
-    recv = None
-    if rank == 0:
-        recv = [[torch.empty_like(bufs[0][k]) for _ in range(world)]
-                for k in ("obs_window", "reward", "traj_done")]
-    nbytes = sum(bufs[0][k].numel() * bufs[0][k].element_size()
-                 for k in ("obs_window", "reward", "traj_done"))
+def time_gather(dist, b, acts, outs, T, WU, K, world, E, N):
+    """Rollout chunks with each chunk's (window obs, reward, done) gathered to rank 0
+    over RCCL on a side stream, overlapped with the next chunk (mapfx.dist)."""
+    from mapfx.dist import OverlappedGather
+    og = OverlappedGather(b, T, keys=("obs_window", "reward", "traj_done"), outputs=outs)
+    og.step_chunk(actions=acts[:T])                  # warm the communicator
+    torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    nl = K // T
-    ev_done = [torch.cuda.Event() for _ in range(2)]
-    for i in range(nl):
-        cur = bufs[i & 1]
-        if i >= 2:
-            torch.cuda.current_stream().wait_event(ev_done[i & 1])
-        b.rollout(T, actions=acts[WU + i * T:WU + (i + 1) * T], traj=cur, outputs=outs)
-        ready = torch.cuda.Event()
-        ready.record()
-        with torch.cuda.stream(side):
-            side.wait_event(ready)
-            for j, k in enumerate(("obs_window", "reward", "traj_done")):
-                dist.gather(cur[k], gather_list=recv[j] if rank == 0 else None, dst=0)
-            ev_done[i & 1].record(side)
+    for i in range(K // T):
+        og.step_chunk(actions=acts[WU + i * T:WU + (i + 1) * T])
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    dist.barrier()
     t = torch.tensor([el], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
     return {"value": round(world * E * N * K / el, 1), "ms_per_step": round(el / K * 1e3, 5),
-            "bytes_per_rank_per_chunk": int(nbytes), "chunk_steps": T,
+            "bytes_per_rank_per_chunk": int(og.bytes_per_chunk()), "chunk_steps": T,
             "collective": "torch.distributed.gather (RCCL) to rank 0 on a side stream"}
 
 
@@ -284,10 +267,12 @@ def cpu_baseline(inst, S, N, E, W, seconds):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=2 ** 31 - 1,
                           nthreads=threads)
+    ob.rollout(2, seed=2, t0=0, window=W)         # thread-pool / page warm-up
+    ob.reset()
     t0 = time.perf_counter()
-    ob.rollout(2, seed=2, t0=0, window=W)
+    ob.rollout(64, seed=2, t0=0, window=W)
     probe = time.perf_counter() - t0
-    steps = int(max(1, min(200000, seconds / max(probe / 2, 1e-6))))
+    steps = int(max(1, min(200000, seconds / max(probe / 64, 1e-6))))
     ob.reset()
     t0 = time.perf_counter()
     ob.rollout(steps, seed=2, t0=0, window=W)

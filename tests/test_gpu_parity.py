@@ -342,3 +342,61 @@ def test_dropin_mapf_grid_on_goldens(mapfx_mod, tmp_path, name):
         env.step([0] * (n + 1))
     with pytest.raises(AssertionError):
         env.step([5] + [0] * (n - 1))
+
+
+# ---------------------------------------------------------------------------
+# 5. env sharding: shards keyed by global env id
+# ---------------------------------------------------------------------------
+def test_sharded_batches_equal_full_batch(mapfx_mod):
+    """Three env_offset shards of uneven size (as mapfx.dist.shard hands to 3
+    ranks) stepped with generator actions equal one unsharded batch, env for env."""
+    from mapfx.dist import shard
+    from mapfx.maps import synthetic_instances
+    E, S, N, T, world = 1000, 32, 16, 40, 3
+    full = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=5)
+    b = mapfx_mod.MapfGridBatch(full["init_pos"], full["goals"], bits=full["bits"], hw=(S, S),
+                                episode_limit=30, obs=("window",))
+    b.reset()
+    ref = b.rollout(T, seed=9, t0=0, autoreset=True)
+    for r in range(world):
+        off, cnt = shard(E, r, world)
+        inst = synthetic_instances(cnt, S, S, N, p_obstacle=0.1, seed=5, env_offset=off)
+        assert np.array_equal(inst["bits"], full["bits"][off:off + cnt])
+        bs = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"],
+                                     hw=(S, S), episode_limit=30, obs=("window",), env_offset=off)
+        bs.reset()
+        tr = bs.rollout(T, seed=9, t0=0, autoreset=True)
+        for k in ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos",
+                  "traj_done", "traj_t"):
+            assert np.array_equal(_np(tr[k]), _np(ref[k])[:, off:off + cnt]), (r, k)
+        assert np.array_equal(_np(bs.pos), _np(b.pos)[off:off + cnt])
+
+
+def test_overlapped_gather_single_rank(mapfx_mod):
+    """OverlappedGather on a 1-rank RCCL group: rank 0's received chunk equals the
+    chunk it stepped, for both double buffers."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from mapfx.dist import OverlappedGather
+    from mapfx.maps import synthetic_instances
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        E, S, N, T = 256, 32, 16, 8
+        inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=2)
+        b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"],
+                                    hw=(S, S), episode_limit=100, obs=("window",))
+        b.reset()
+        og = OverlappedGather(b, T)
+        for i in range(3):
+            tr = og.step_chunk(seed=4, t0=i * T)
+            og.synchronize()
+            for k in og.keys:
+                assert torch.equal(og.recv[k][0], tr[k]), (i, k)
+    finally:
+        dist.destroy_process_group()

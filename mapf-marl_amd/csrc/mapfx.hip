@@ -84,6 +84,7 @@ struct Geo {
   uint64_t m_wpr;          // fastdiv magic for words-per-padded-row
   uint64_t m_W;            // fastdiv magic for W
   uint64_t m_W4;           // fastdiv magic for W/4
+  uint64_t m_pitch;        // fastdiv magic for the padded pitch (cells)
   int wpr;
   // LDS regions (byte offsets from the dynamic LDS base)
   int off_map, off_bits, off_oldc, off_newc, off_rc, off_goal, off_rew, off_flag, off_stage;
@@ -586,6 +587,41 @@ __device__ unsigned long long g_stamps[256 * 8];
   } while (0)
 #endif
 
+// Padded u8 cell map of one env from its LDS bitmap, one map row per lane at a
+// time: border rows / pad words are constant, an interior word is one 4-bit
+// window of the bitmap row spread to the four cells' obstacle flags.  No
+// division and no per-word bounds tests.
+__device__ inline void build_map_rows_u8(const Geo& g, uint32_t* map32, const uint32_t* bitsL,
+                                         int lane, int nl) {
+  const int wpr = g.wpr, plw = g.pl >> 2;
+  const int iw = (g.W + 3) >> 2;  // interior words (the last one may hold border cells)
+  const uint32_t last_or = (g.W & 3) ? ((0xFu << (g.W & 3)) & 0xFu) : 0u;
+  for (int pr = lane; pr < g.rows; pr += nl) {
+    uint32_t* row = map32 + pr * wpr;
+    const int rr = pr - g.P;
+    if (rr < 0 || rr >= g.H) {
+      for (int w = 0; w < wpr; ++w) row[w] = 0x80808080u;
+      continue;
+    }
+    for (int w = 0; w < plw; ++w) row[w] = 0x80808080u;
+    // 32 cells (8 map words) per bitmap read pair: the reads of a chunk are waited
+    // for once, not once per word
+    for (int k0 = 0; k0 < iw; k0 += 8) {
+      const int p = rr * g.W + 4 * k0;
+      const uint32_t x = __builtin_amdgcn_alignbit(bitsL[(p >> 5) + 1], bitsL[p >> 5], p & 31);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (k0 + j < iw) {
+          uint32_t nib = (x >> (4 * j)) & 0xFu;
+          if (k0 + j == iw - 1) nib |= last_or;
+          row[plw + k0 + j] = ((nib * 0x00204081u) & 0x01010101u) * 0x80u;
+        }
+      }
+    }
+    for (int w = plw + iw; w < wpr; ++w) row[w] = 0x80808080u;
+  }
+}
+
 __device__ inline void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -722,46 +758,66 @@ __device__ __forceinline__ void stage_record(const uint32_t (&R)[4 * WIN], unsig
 // FULLW: every lane owns an agent (N == L and E % EPW == 0) -> no lane masks.
 // RUNNER (rollout only): the standard runner outputs are all present (reward,
 // term, node, edge, avail, traj_pos/done/t, window obs) -> no per-output tests.
-// Rollouts software-pipeline each step's tail (fp64 fold, env outputs, window
-// copy-out; double-buffered rew/staging) into the next step's LDS latencies.
-template <int WIN, bool ROLL, bool FULLW, bool RUNNER>
+// LL: lanes per env fixed at compile time (0: g.L at run time); with FULLW, N == LL.
+//
+// Software pipeline (one wave, in-order LDS).  Iteration s runs
+//   A  step s's move decision from the carried neighbour bytes, its `dep` write and
+//      count atomics                                            (dependency chain)
+//   B  issue of step s's post-step window rows, the occupant's move, and the
+//      previous-but-one step's reward row (fp64 fold)
+//   C  the HEAVY part of step s-1 from registers saved in iteration s-1: window
+//      SWAR, record and per-agent stores, node/edge collisions, fp64 reward, and
+//      the env outputs of step s-2 -- VALU work that fills B's LDS latency
+//   D  step s's neighbour bytes, dones, t and all-done ballot  (dependency chain)
+// so only A and D (a few dozen instructions) sit on the serial chain between
+// steps.  The last step's heavy part and tails run after the loop.
+template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL>
 __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   extern __shared__ __align__(16) unsigned char lds[];
   constexpr int WW = WIN * WIN;
   constexpr int H2 = WIN / 2;
   constexpr int REC = 2 * WW;  // record bytes per agent
+  constexpr int NX = WIN > 0 ? WIN : 1;
+  constexpr bool FIXN = FULLW && LL > 0;   // N == LL known at compile time
+  constexpr bool FLAT = RUNNER && FULLW;   // env outputs stored by every lane of the env
+  const int L = LL > 0 ? LL : g.L;
+  const int lshift = LL > 0 ? (LL == 64 ? 6 : LL == 32 ? 5 : LL == 16 ? 4 : LL == 8 ? 3 : LL == 4 ? 2 : LL == 2 ? 1 : 0)
+                            : g.lshift;
   const int lane64 = threadIdx.x;
-  const int slot = lane64 >> g.lshift;  // env slot within the wave
-  const int ag = lane64 & (g.L - 1);    // agent index
-  const int base = slot << g.lshift;    // first lane of this env
-  const int env0 = blockIdx.x * g.EPW;
+  const int slot = lane64 >> lshift;  // env slot within the wave
+  const int ag = lane64 & (L - 1);    // agent index
+  const int base = slot << lshift;    // first lane of this env
+  const int EPW = 64 >> lshift;
+  const int env0 = blockIdx.x * EPW;
   const int env = env0 + slot;
-  const int N = g.N;
+  const int N = FIXN ? LL : g.N;
   const bool env_ok = FULLW || env < g.E;
   const bool has = FULLW || (env_ok && ag < N);
   const bool do_step = ROLL || a.do_step;
-  const uint64_t envmask = (g.L == 64 ? ~0ull : ((1ull << g.L) - 1ull)) << base;
+  const uint64_t envmask = (L == 64 ? ~0ull : ((1ull << L) - 1ull)) << base;
   const int pitch = g.pitch;
   const int Wd = g.W;
   const bool want_win = WIN > 0 && (RUNNER || a.obs_window);
-  const int nenv = FULLW ? g.EPW : min(g.EPW, g.E - env0);
+  const int nenv = FULLW ? EPW : min(EPW, g.E - env0);
+  const int cell0 = g.P * pitch + g.pl;  // padded index of cell (0, 0)
 
   unsigned char* map = lds + g.wv_off_map + slot * g.map_env_bytes;
   uint32_t* map32 = (uint32_t*)map;
   unsigned char* dep = lds + g.wv_off_dep + slot * g.map_env_bytes;  // move dir per old cell
   uint32_t* bitsL = (uint32_t*)(lds + g.wv_off_bits + slot * g.wv_bits_env_bytes);
+  double* rewL = (double*)(lds + g.wv_off_rew);
+  const int rew_buf = g.wv_rew_buf / 8;  // doubles per reward buffer
+  const int rew_row = g.wv_rew_row;      // doubles per env row
 
   const uint32_t oa = (uint32_t)(env * N + ag);  // agent index inside one step slot
   const uint32_t EN = (uint32_t)(g.E * N);
-  int r = 0, c = 0, gr = 0, gc = 0, st = 0;
+  int cur = 0, gcell = -1, st = 0;  // padded cell of the agent / of its goal
   bool dn = false;
   if (has) {
     const int2 p = ((const int2*)a.pos)[oa];
     const int2 q = ((const int2*)a.goal)[oa];
-    r = p.x;
-    c = p.y;
-    gr = q.x;
-    gc = q.y;
+    cur = cell0 + p.x * pitch + p.y;
+    gcell = cell0 + q.x * pitch + q.y;
     dn = a.done[oa] != 0;
     if (a.steps) st = a.steps[oa];
   }
@@ -769,49 +825,47 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   const int T = ROLL ? a.T : 1;
   // Actions are fetched for AB steps at a time: one VMEM wait per block instead of
   // one per step (a wait on a per-step load would also drain the step's stores).
-  constexpr int AB = ROLL ? 16 : 1;
+#ifndef MAPFX_AB
+#define MAPFX_AB 16
+#endif
+  constexpr int AB = ROLL ? MAPFX_AB : 1;
   uint32_t actpk[(AB + 3) / 4];
 
   // ---- bitmap -> LDS, padded map, agents ----
   if (env_ok) {
     const uint32_t* src =
         (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)env * g.map_stride));
-    for (int w = ag; w < g.bits_words; w += g.L) bitsL[w] = src[w];
+    for (int w = ag; w < g.bits_words; w += L) bitsL[w] = src[w];
+  }
+  if (ROLL) {  // both reward rows start at +0.0 (folds of steps < 0 read them)
+    for (int i = lane64; i < 2 * rew_buf; i += 64) rewL[i] = 0.0;
   }
   wave_fence();
-  for (int wi = ag; wi < g.map_words; wi += g.L) {
-    const int pr = fastdiv(wi, g.m_wpr);
-    const int pw = wi - pr * g.wpr;
-    const int rr = pr - g.P;
-    const int c0 = pw * 4 - g.pl;
-    uint32_t word = 0x80808080u;
-    if (rr >= 0 && rr < g.H && c0 >= 0 && c0 < Wd) {
-      const int p = rr * Wd + c0;
-      const uint32_t w0 = bitsL[p >> 5], w1 = bitsL[(p >> 5) + 1];
-      uint32_t nib = __builtin_amdgcn_alignbit(w1, w0, p & 31) & 0xFu;
-      if (c0 + 4 > Wd) nib |= (0xFu << (Wd - c0)) & 0xFu;  // right border cells
-      word = ((nib * 0x00204081u) & 0x01010101u) * 0x80u;
-    }
-    map32[wi] = word;
-  }
+  build_map_rows_u8(g, map32, bitsL, ag, L);
   wave_fence();
-  if (has) {
-    const int oc = (r + g.P) * pitch + c + g.pl;
-    atomicAdd(&map32[oc >> 2], 1u << ((oc & 3) * 8));
-  }
+  if (has) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
   wave_fence();
 
-  // tail of step s (fold, env outputs, window copy-out) — runs one step late in rollouts
-  // rewards of a step are folded from LDS (rew[buf]: one row of N fp64 per env,
-  // padded with +0.0 to a multiple of 2; adding +0.0 never changes a sum that
-  // starts at +0.0) -- as 16 independent-of-this-step adds the scheduler can
-  // interleave with the window work.
-  const int rew_row = g.wv_rew_row;  // doubles per env row
+  const auto cell_rc = [&](int cell) {  // padded cell -> (row, col)
+    const int pr = fastdiv(cell, g.m_pitch);
+    return make_int2(pr - g.P, cell - pr * pitch - g.pl);
+  };
+  // `sum(rewards)`: naive left fold in agent order (:141) over the env's LDS row
+  // (padded with +0.0: adding +0.0 never changes a sum that starts at +0.0)
   auto fold = [&](int buf) {
-    const double* rw = (const double*)(lds + g.wv_off_rew + buf * g.wv_rew_buf) + slot * rew_row;
-    double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
+    const double* rw = rewL + buf * rew_buf + slot * rew_row;
+    double R = 0.0;
     if (MAPFX_ABLATE & 2) return R;
-    if (g.L == 16) {  // all 16 lanes wrote their slot (+0.0 past N)
+    if constexpr (FIXN) {
+#pragma unroll
+      for (int j0 = 0; j0 < LL; j0 += 16) {
+        double v[LL < 16 ? LL : 16];
+#pragma unroll
+        for (int j = 0; j < (LL < 16 ? LL : 16); ++j) v[j] = rw[j0 + j];
+#pragma unroll
+        for (int j = 0; j < (LL < 16 ? LL : 16); ++j) R = R + v[j];
+      }
+    } else if (L == 16) {  // all 16 lanes wrote their slot (+0.0 past N)
       double v[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) v[j] = rw[j];
@@ -822,10 +876,14 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
     }
     return R;
   };
-  // tail of step s (env outputs, window copy-out) -- runs one step late in rollouts
+  // env outputs of a step: reward, term, t, f32 copy, error flag, staged window copy-out
   auto tail = [&](int buf, uint32_t se_t, bool skip_t, bool alldone_t, int tcur_t, double R) {
-    if (env_ok && ag == 0) {
-      const uint32_t ei = se_t + env;
+    const uint32_t ei = se_t + env;
+    if (FLAT) {  // every lane of the env stores the same values: no lane branch
+      a.reward[ei] = R;
+      a.term[ei] = alldone_t ? 1 : 0;
+      a.traj_t[ei] = tcur_t;
+    } else if (env_ok && ag == 0) {
       if (RUNNER) {
         a.reward[ei] = R;
         a.term[ei] = alldone_t ? 1 : 0;
@@ -835,6 +893,8 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
         if (a.term) a.term[ei] = alldone_t ? 1 : 0;
         if (a.traj_t) a.traj_t[ei] = tcur_t;
       }
+    }
+    if (env_ok && ag == 0) {
       if (do_step && a.reward_f32) a.reward_f32[ei] = (float)R;
       if (do_step && a.err && skip_t) atomicCAS(a.err, 0, env + 1);
     }
@@ -851,26 +911,112 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
     }
   };
 
+  // ---- state of step q = s-1 saved for its heavy part (C) ----
+  uint32_t qx[3 * NX];  // window rows: [xlo | xhi | xhi2] (WIN == 0: 5 neighbour bytes)
+  int q_oc = 0, q_nc = 0, q_act = 4, q_pre = 0, q_tcur = 0;
+  uint32_t q_dj = 0xFFu, q_nb = 0;
+  bool q_moved = false, q_envc = false, q_dnold = false, q_dn = false, q_live = false;
+  bool q_skip = false, q_alldone = false;
+  // ---- env outputs of step p = s-2 waiting for their fold ----
   uint32_t p_se = 0;
   bool p_skip = false, p_alldone = false;
   int p_tcur = 0;
+
+  // HEAVY part of step q (slot qs): window, node, edge, reward, per-agent stores.
+  auto heavy = [&](int qs) {
+    const uint32_t so = ROLL ? (uint32_t)qs * EN : 0u;
+    const int buf = ROLL ? (qs & 1) : 0;
+    uint32_t node = 0;
+    uint32_t R[WIN > 0 ? 4 * WIN : 1];  // [plane][cols 0-3 | cols 4-7][row]
+    if constexpr (WIN > 0) {
+      const int o = (q_nc - H2) & 3;  // same byte offset in every row (pitch % 4 == 0)
+      uint32_t X0[WIN], X1[WIN];
+#pragma unroll
+      for (int y = 0; y < WIN; ++y) {
+        X0[y] = __builtin_amdgcn_alignbyte(qx[WIN + y], qx[y], o);           // cells 0-3
+        X1[y] = __builtin_amdgcn_alignbyte(qx[2 * WIN + y], qx[WIN + y], o);  // cells 4-7
+        swar_window(X0[y], R[y], R[2 * WIN + y]);
+        R[WIN + y] = R[3 * WIN + y] = 0;
+        if (WIN > 4) swar_window(X1[y], R[WIN + y], R[3 * WIN + y]);
+      }
+      const uint32_t ctr = ((H2 >= 4 ? X1[H2] : X0[H2]) >> (8 * (H2 & 3))) & 0x7Fu;
+      node = ctr > 1u ? 1u : 0u;
+    } else {
+      node = (qx[0] & 0x7Fu) > 1u ? 1u : 0u;
+    }
+    if (q_skip) node = 0;
+    uint32_t availm = 16u;  // avail (:203-224): neighbour not (obstacle, 0 agents)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) availm |= (((q_nb >> (8 * d)) & 0xFFu) != 0x80u) ? (1u << d) : 0u;
+    if constexpr (WIN > 0) {
+      if (want_win && has && !(MAPFX_ABLATE & 1)) {
+#if MAPFX_DIRECT_REC
+        write_record<WIN>(R, (unsigned char*)a.obs_window + (size_t)(so + oa) * REC);
+#else
+        stage_record<WIN>(R, lds + g.wv_off_stage + buf * g.wv_stage_buf +
+                                 (uint32_t)(slot * N + ag) * REC);  // -> LDS staging
+#endif
+      }
+    }
+    const uint32_t ai = so + oa;
+    if (has && !(MAPFX_ABLATE & 8)) {
+      const int2 rc = cell_rc(q_nc);
+      if (RUNNER) {
+        a.node[ai] = (uint8_t)node;
+        ((int2*)a.traj_pos)[ai] = rc;
+        a.traj_done[ai] = q_dn ? 1 : 0;
+        a.avail[ai] = (uint8_t)availm;
+      } else {
+        if (do_step && a.node) a.node[ai] = (uint8_t)node;
+        if (a.traj_pos) ((int2*)a.traj_pos)[ai] = rc;
+        if (a.traj_done) a.traj_done[ai] = q_dn ? 1 : 0;
+        if (a.avail) a.avail[ai] = (uint8_t)availm;
+      }
+    }
+    // edge collisions (:364-383): i moved into a cell X that had pre-step
+    // occupants; j counts iff j moved from X back into i's old cell, i.e. in the
+    // opposite direction (act ^ 1)
+    int edge = 0;
+    const bool suspect = q_moved && q_pre > 0;
+    if (__ballot(suspect)) {
+      if (suspect && q_pre == 1) edge = q_dj == (uint32_t)(q_act ^ 1) ? 1 : 0;
+      if (__ballot(suspect && q_pre > 1)) {  // stacked pre-occupants: scan the env
+        for (int j = 0; j < N; ++j) {
+          const int oj2 = __shfl(q_oc, base + j);
+          const int nj2 = __shfl(q_nc, base + j);
+          if (suspect && q_pre > 1) edge += (oj2 == q_nc) & (nj2 == q_oc);
+        }
+      }
+    }
+    // reward (:94-130, exact fp64 op order)
+    double rr = 0.0;
+    if (q_live) {
+      if (!q_dnold) {
+        if (q_envc) rr = rr + g.collide_rew;
+        rr = rr + g.step_rew;
+      }
+      rr = rr + g.collide_rew * (double)node;
+      rr = rr + g.collide_rew * (double)edge;
+    }
+    if (do_step && (FIXN || ag < rew_row))  // lanes past N pad the row with +0.0
+      rewL[buf * rew_buf + slot * rew_row + ag] = has ? rr : 0.0;
+    if (has && !(MAPFX_ABLATE & 8)) {
+      if (RUNNER || (do_step && a.edge)) a.edge[ai] = (uint8_t)(edge > 255 ? 255 : edge);
+    }
+  };
+
   // Retire the state loads here (s_waitcnt vmcnt(0), gfx9 encoding): otherwise the
   // waitcnt pass merges "load pending" into the loop header and re-waits vmcnt(0)
-  // -- i.e. drains every outstanding store -- at each use of r/c/t inside the loop.
+  // -- i.e. drains every outstanding store -- at each use of the state inside the loop.
   __builtin_amdgcn_s_waitcnt(0x0F70);
   // Raw map bytes of the 4 neighbours (byte d = cell of action d), carried from the
   // end of one step (post-step map) to the move decision of the next (pre-step
   // map): the move test needs no LDS round trip.
   uint32_t nb = 0;
-  if (has) {
-    const int oc = (r + g.P) * pitch + c + g.pl;
-    nb = (uint32_t)map[oc - pitch] | ((uint32_t)map[oc + pitch] << 8) |
-         ((uint32_t)map[oc - 1] << 16) | ((uint32_t)map[oc + 1] << 24);
-  }
+  if (has)
+    nb = (uint32_t)map[cur - pitch] | ((uint32_t)map[cur + pitch] << 8) |
+         ((uint32_t)map[cur - 1] << 16) | ((uint32_t)map[cur + 1] << 24);
   for (int s = 0; s < T; ++s) {
-    const uint32_t so = ROLL ? (uint32_t)s * EN : 0u;            // step slot (agents)
-    const uint32_t se = ROLL ? (uint32_t)s * (uint32_t)g.E : 0u;  // step slot (envs)
-    const int buf = ROLL ? (s & 1) : 0;
     if ((s & (AB - 1)) == 0) {  // actions of steps s .. s+AB-1, packed 4 per u32
       int v[AB];
       if (!do_step) {  // observation pass: there is no action buffer
@@ -906,147 +1052,85 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
       actpk[k] = (k + 1 < (AB + 3) / 4) ? __builtin_amdgcn_alignbit(actpk[k + 1], actpk[k], 8)
                                         : (actpk[k] >> 8);
     STAMP(0);
-    // ---------------- move decision on the PRE-step map (:319-342) ----------------
-    const int oc = (r + g.P) * pitch + c + g.pl;
-    const bool bad_l = act == 0xFF;
-    const bool mv = !dn && !bad_l && act != 4;  // (!has / observe lanes carry act == 4)
-    const int cand = oc + (act == 0 ? -pitch : (act == 1 ? pitch : (act == 2 ? -1 : 1)));
-    const uint32_t v = mv ? ((nb >> (8 * (act & 3))) & 0xFFu) : 0x80u;  // pre-step cell
-    STAMP(7);
-    STAMP(1);
+    // ---------------- A: move decision on the PRE-step map (:319-342) ----------------
+    const int oc = cur;
+    const bool mv = !dn && (uint32_t)act < 4u;  // 4 = stay, 0xFF = invalid (!has: 4)
+    const uint32_t v = mv ? ((nb >> ((act & 3) * 8)) & 0xFFu) : 0x80u;  // pre-step cell
     const bool envc = mv && v == 0x80u;  // out of bounds / free-standing obstacle (quirk 1)
-    const bool skip = !do_step || ((__ballot(bad_l) & envmask) != 0);
+    const bool skip = !do_step || ((__ballot(act == 0xFF) & envmask) != 0);
     const bool moved = mv && v != 0x80u && !skip;
-    const int pre = (int)(v & 0x7Fu);
-    const int nc = moved ? cand : oc;
+    int dlt = (act & 2) ? 1 : pitch;  // 0: up, 1: down, 2: left, 3: right
+    dlt = (act & 1) ? dlt : -dlt;
+    const int nc = moved ? oc + dlt : oc;
     if (has && !(MAPFX_ABLATE & 64)) dep[oc] = moved ? (unsigned char)act : (unsigned char)0xFF;
-    if (moved) {
-      if (!(MAPFX_ABLATE & 16)) {
+    if (!(MAPFX_ABLATE & 16)) {
+      if (FULLW) {  // branch-free: lanes that stay add 0 to their own cell's word
+        atomicAdd(&map32[oc >> 2], moved ? 0u - (1u << ((oc & 3) * 8)) : 0u);
+        atomicAdd(&map32[nc >> 2], moved ? 1u << ((nc & 3) * 8) : 0u);
+      } else if (moved) {
         atomicSub(&map32[oc >> 2], 1u << ((oc & 3) * 8));
         atomicAdd(&map32[nc >> 2], 1u << ((nc & 3) * 8));
       }
-      r += act_dr(act);
-      c += act_dc(act);
     }
+    cur = nc;
     STAMP(2);
-    // ---------------- edge collisions (:364-383) ----------------
-    // i moved into a cell X that had pre-step occupants; j counts iff j moved from
-    // X back into i's old cell, i.e. in the opposite direction (act ^ 1).
-    // POST-step rows of the window (or the 4 neighbours), the occupant's move, and
-    // the previous step's tail are all issued before any of them is waited for.
-    uint32_t xlo[WIN > 0 ? WIN : 1], xhi[WIN > 0 ? WIN : 1], xhi2[WIN > 0 ? WIN : 1];
-    uint32_t nbw[4];
+    // ---------------- B: issue step s's rows, occupant move, fold of step s-2 -------
+    uint32_t x[3 * NX];
     if constexpr (WIN > 0) {
+      const int w0 = (nc - H2 * pitch - H2) >> 2;
+      const int wpr = pitch >> 2;
 #pragma unroll
       for (int y = 0; y < WIN; ++y) {
-        const int wb = (nc + (y - H2) * pitch - H2) >> 2;
-        xlo[y] = map32[wb];
-        xhi[y] = map32[wb + 1];
-        xhi2[y] = WIN > 5 ? map32[wb + 2] : 0u;
+        x[y] = map32[w0 + y * wpr];
+        x[WIN + y] = map32[w0 + y * wpr + 1];
+        x[2 * WIN + y] = WIN > 5 ? map32[w0 + y * wpr + 2] : 0u;
       }
     } else if (!(MAPFX_ABLATE & 32)) {
-      nbw[0] = map[nc - pitch];
-      nbw[1] = map[nc + pitch];
-      nbw[2] = map[nc - 1];
-      nbw[3] = map[nc + 1];
-      nbw[0] |= (uint32_t)map[nc] << 8;  // centre (node) in byte 1 of nbw[0]
+      x[0] = map[nc];  // centre (node), then up / down / left / right
+      x[1] = map[nc - pitch];
+      x[2] = map[nc + pitch];
     } else {
-      nbw[0] = nbw[1] = nbw[2] = nbw[3] = 1u;
+      x[0] = x[1] = x[2] = 1u;
+    }
+    uint32_t xl = 0, xr = 0;
+    if constexpr (WIN == 0) {
+      xl = map[nc - 1];
+      xr = map[nc + 1];
     }
     const uint32_t dj = (MAPFX_ABLATE & 64) ? 0xFFu : dep[nc];  // pre-step occupant's move
-    const double R_prev = (ROLL && s > 0 && do_step) ? fold(buf ^ 1) : 0.0;
-    if (ROLL && s > 0) tail(buf ^ 1, p_se, p_skip, p_alldone, p_tcur, R_prev);
-    int edge = 0;
-    const bool suspect = moved && pre > 0;
-    if (__ballot(suspect)) {
-      if (suspect && pre == 1) edge = dj == (uint32_t)(act ^ 1) ? 1 : 0;
-      if (__ballot(suspect && pre > 1)) {  // stacked pre-occupants: scan the env
-        for (int j = 0; j < N; ++j) {
-          const int oj2 = __shfl(oc, base + j);
-          const int nj2 = __shfl(nc, base + j);
-          if (suspect && pre > 1) edge += (oj2 == nc) & (nj2 == oc);
-        }
-      }
-    }
+    const double Rp = (ROLL && do_step) ? fold(s & 1) : 0.0;     // step s-2's row
+    // ---------------- C: heavy part of step s-1, env outputs of step s-2 -----------
+    if (s > 0) heavy(s - 1);
+    if (ROLL && s > 1) tail(s & 1, p_se, p_skip, p_alldone, p_tcur, Rp);
     STAMP(3);
-    // ---------------- POST-step map rows: window, node, avail ----------------
-    uint32_t node = 0, availm = 16u;
-    uint32_t R[WIN > 0 ? 4 * WIN : 1];  // [plane][cols 0-3 | cols 4-7][row]
+    // ---------------- D: step s's neighbours, dones, t (:112-117) ----------------
+    uint32_t nbn;
     if constexpr (WIN > 0) {
-      uint32_t X0[WIN], X1[WIN];
-#pragma unroll
-      for (int y = 0; y < WIN; ++y) {
-        const int o = (nc + (y - H2) * pitch - H2) & 3;
-        X0[y] = __builtin_amdgcn_alignbyte(xhi[y], xlo[y], o);   // cells 0-3 of the row
-        X1[y] = __builtin_amdgcn_alignbyte(xhi2[y], xhi[y], o);  // cells 4-7
-        swar_window(X0[y], R[y], R[2 * WIN + y]);
-        R[WIN + y] = R[3 * WIN + y] = 0;
-        if (WIN > 4) swar_window(X1[y], R[WIN + y], R[3 * WIN + y]);
-      }
-      const auto raw = [&](int y, int x) { return ((x >= 4 ? X1[y] : X0[y]) >> (8 * (x & 3))) & 0xFFu; };
-      node = (raw(H2, H2) & 0x7Fu) > 1u ? 1u : 0u;
-      nb = raw(H2 - 1, H2) | (raw(H2 + 1, H2) << 8) | (raw(H2, H2 - 1) << 16) | (raw(H2, H2 + 1) << 24);
+      // the 4 neighbours lie in the first 8 bytes of their window rows (o + H2 + 1 <= 7)
+      const int o8 = ((nc - H2) & 3) * 8;
+      const auto row64 = [&](int y) { return ((uint64_t)x[WIN + y] << 32) | x[y]; };
+      const uint32_t up = (uint32_t)(row64(H2 - 1) >> (o8 + 8 * H2)) & 0xFFu;
+      const uint32_t dw = (uint32_t)(row64(H2 + 1) >> (o8 + 8 * H2)) & 0xFFu;
+      const uint32_t cr = (uint32_t)(row64(H2) >> (o8 + 8 * (H2 - 1)));  // left, centre, right
+      nbn = up | (dw << 8) | ((cr & 0xFFu) << 16) | (((cr >> 16) & 0xFFu) << 24);
     } else {
-      node = ((nbw[0] >> 8) & 0x7Fu) > 1u ? 1u : 0u;
-      nb = (nbw[0] & 0xFFu) | (nbw[1] << 8) | (nbw[2] << 16) | (nbw[3] << 24);
+      nbn = (x[1] & 0xFFu) | ((x[2] & 0xFFu) << 8) | ((xl & 0xFFu) << 16) | ((xr & 0xFFu) << 24);
     }
-    // avail (:203-224): a neighbour is available iff it is not (obstacle, 0 agents)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) availm |= (((nb >> (8 * d)) & 0xFFu) != 0x80u) ? (1u << d) : 0u;
-    if (skip) node = 0;
-    STAMP(4);
-    // ---------------- reward (:94-130, exact fp64 op order) and dones ----------------
-    double rr = 0.0;
-    if (!skip && !(MAPFX_ABLATE & 128)) {
-      if (!dn) {
-        if (envc) rr = rr + g.collide_rew;
-        rr = rr + g.step_rew;
-        ++st;
-      }
-      rr = rr + g.collide_rew * (double)node;
-      rr = rr + g.collide_rew * (double)edge;
-      if (r == gr && c == gc) dn = true;   // :112-114
-      if (tcur + 1 >= g.limit) dn = true;  // :116-117 (t is incremented below)
-    }
-    if (do_step && ag < rew_row)  // lanes past N pad the row with +0.0
-      ((double*)(lds + g.wv_off_rew + buf * g.wv_rew_buf))[slot * rew_row + ag] = has ? rr : 0.0;
+    const bool dn_old = dn;
+    const bool live = !skip && !(MAPFX_ABLATE & 128);
+    if (live && nc == gcell) dn = true;          // :112-114 (goal reached)
+    if (live && tcur + 1 >= g.limit) dn = true;  // :116-117 (t is incremented below)
+    if (live && !dn_old) ++st;
     if (!skip) ++tcur;
     const bool alldone = (__ballot(has && !dn) & envmask) == 0;
-    if constexpr (WIN > 0) {
-      if (want_win && has && !(MAPFX_ABLATE & 1)) {
-#if MAPFX_DIRECT_REC
-        write_record<WIN>(R, (unsigned char*)a.obs_window + (size_t)(so + oa) * REC);
-#else
-        stage_record<WIN>(R, lds + g.wv_off_stage + buf * g.wv_stage_buf +
-                                 (uint32_t)(slot * N + ag) * REC);  // -> LDS staging
-#endif
-      }
-    }
-    // ---------------- per-agent outputs ----------------
-    if (has && !(MAPFX_ABLATE & 8)) {
-      const uint32_t ai = so + oa;
-      if (RUNNER) {
-        a.node[ai] = (uint8_t)node;
-        a.edge[ai] = (uint8_t)(edge > 255 ? 255 : edge);
-        ((int2*)a.traj_pos)[ai] = make_int2(r, c);
-        a.traj_done[ai] = dn ? 1 : 0;
-        a.avail[ai] = (uint8_t)availm;
-      } else {
-        if (do_step) {
-          if (a.node) a.node[ai] = (uint8_t)node;
-          if (a.edge) a.edge[ai] = (uint8_t)(edge > 255 ? 255 : edge);
-        }
-        if (a.traj_pos) ((int2*)a.traj_pos)[ai] = make_int2(r, c);
-        if (a.traj_done) a.traj_done[ai] = dn ? 1 : 0;
-        if (a.avail) a.avail[ai] = (uint8_t)availm;
-      }
-    }
-    if (!RUNNER && a.obs_full && env_ok) {  // :143-192, row-major occ = count - flag
+    if (!RUNNER && a.obs_full && env_ok) {  // :143-192, row-major occ = count - flag (now:
+      // the next step's atomics would change the map)
+      const uint32_t se = ROLL ? (uint32_t)s * (uint32_t)g.E : 0u;
       unsigned char* outb = (unsigned char*)a.obs_full + (size_t)(se + env) * g.H * Wd;
       if ((Wd & 3) == 0) {
         const int wpr_out = Wd >> 2;
         const int nwords = g.H * wpr_out;
-        for (int i = ag; i < nwords; i += g.L) {
+        for (int i = ag; i < nwords; i += L) {
           const int rr_ = fastdiv(i, g.m_W4);
           const int cw = i - rr_ * wpr_out;
           const uint32_t vv = map32[((rr_ + g.P) * pitch + g.pl) / 4 + cw];
@@ -1054,7 +1138,7 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
           ((uint32_t*)outb)[i] = (((vv & 0x7F7F7F7Fu) | 0x80808080u) - f) ^ 0x80808080u;
         }
       } else {
-        for (int i = ag; i < g.H * Wd; i += g.L) {
+        for (int i = ag; i < g.H * Wd; i += L) {
           const int rr_ = fastdiv(i, g.m_W);
           const int cc_ = i - rr_ * Wd;
           const uint32_t vv = map[(rr_ + g.P) * pitch + cc_ + g.pl];
@@ -1062,41 +1146,59 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
         }
       }
     }
-    wave_fence();
-    STAMP(6);
-    p_se = se;
-    p_skip = skip;
-    p_alldone = alldone;
-    p_tcur = tcur;
-    if (!ROLL) {
-      wave_fence();
-      tail(buf, se, skip, alldone, tcur, do_step ? fold(buf) : 0.0);
-    }
+    // save step s for its heavy part / tail
+    p_se = ROLL ? (uint32_t)(s - 1) * (uint32_t)g.E : 0u;
+    p_skip = q_skip;
+    p_alldone = q_alldone;
+    p_tcur = q_tcur;
+#pragma unroll
+    for (int i = 0; i < 3 * NX; ++i) qx[i] = x[i];
+    q_oc = oc;
+    q_nc = nc;
+    q_act = act;
+    q_pre = (int)(v & 0x7Fu);
+    q_dj = dj;
+    q_nb = nbn;
+    q_moved = moved;
+    q_envc = envc;
+    q_dnold = dn_old;
+    q_dn = dn;
+    q_live = live;
+    q_skip = skip;
+    q_alldone = alldone;
+    q_tcur = tcur;
+    nb = nbn;
     if (ROLL && a.autoreset && alldone) {
       if (has) {
         const int2 p = ((const int2*)a.init_pos)[oa];
-        const int ocell = (r + g.P) * pitch + c + g.pl;
-        const int ncell = (p.x + g.P) * pitch + p.y + g.pl;
-        atomicSub(&map32[ocell >> 2], 1u << ((ocell & 3) * 8));
+        const int ncell = cell0 + p.x * pitch + p.y;
+        atomicSub(&map32[cur >> 2], 1u << ((cur & 3) * 8));
         atomicAdd(&map32[ncell >> 2], 1u << ((ncell & 3) * 8));
-        r = p.x;
-        c = p.y;
+        cur = ncell;
         dn = false;
         st = 0;
       }
       tcur = 0;
       wave_fence();
-      if (has) {
-        const int o2 = (r + g.P) * pitch + c + g.pl;
-        nb = (uint32_t)map[o2 - pitch] | ((uint32_t)map[o2 + pitch] << 8) |
-             ((uint32_t)map[o2 - 1] << 16) | ((uint32_t)map[o2 + 1] << 24);
-      }
+      if (has)
+        nb = (uint32_t)map[cur - pitch] | ((uint32_t)map[cur + pitch] << 8) |
+             ((uint32_t)map[cur - 1] << 16) | ((uint32_t)map[cur + 1] << 24);
     }
     wave_fence();
+    STAMP(6);
   }
-  if (ROLL && T > 0) tail((T - 1) & 1, p_se, p_skip, p_alldone, p_tcur, fold((T - 1) & 1));
+  // ---- drain the pipeline: heavy part of the last step, the last two tails ----
+  if (T > 0) {
+    const double Rp = (ROLL && T > 1) ? fold(T & 1) : 0.0;  // step T-2's row
+    heavy(T - 1);
+    if (ROLL && T > 1) tail(T & 1, p_se, p_skip, p_alldone, p_tcur, Rp);
+    wave_fence();
+    const int lb = ROLL ? ((T - 1) & 1) : 0;
+    const double Rl = do_step ? fold(lb) : 0.0;
+    tail(lb, ROLL ? (uint32_t)(T - 1) * (uint32_t)g.E : 0u, q_skip, q_alldone, q_tcur, Rl);
+  }
   if (has) {
-    ((int2*)a.pos)[oa] = make_int2(r, c);
+    ((int2*)a.pos)[oa] = cell_rc(cur);
     a.done[oa] = dn ? 1 : 0;
     if (a.steps) a.steps[oa] = st;
   }
@@ -1186,20 +1288,26 @@ int check_hip(hipError_t e, const char* what) {
 }
 
 template <int WIN>
-KernelFn pick_wave_win(bool roll, bool fullw, bool runner) {
+KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L) {
   if (roll) {
-    if (runner) return fullw ? mapf_wave_kernel<WIN, true, true, true> : mapf_wave_kernel<WIN, true, false, true>;
-    return fullw ? mapf_wave_kernel<WIN, true, true, false> : mapf_wave_kernel<WIN, true, false, false>;
+    if (runner) {
+      if (!fullw) return mapf_wave_kernel<WIN, true, false, true, 0>;
+      if (L == 16) return mapf_wave_kernel<WIN, true, true, true, 16>;
+      if (L == 64) return mapf_wave_kernel<WIN, true, true, true, 64>;
+      return mapf_wave_kernel<WIN, true, true, true, 0>;
+    }
+    return fullw ? mapf_wave_kernel<WIN, true, true, false, 0> : mapf_wave_kernel<WIN, true, false, false, 0>;
   }
-  return fullw ? mapf_wave_kernel<WIN, false, true, false> : mapf_wave_kernel<WIN, false, false, false>;
+  if (fullw && L == 16) return mapf_wave_kernel<WIN, false, true, false, 16>;
+  return fullw ? mapf_wave_kernel<WIN, false, true, false, 0> : mapf_wave_kernel<WIN, false, false, false, 0>;
 }
 
-KernelFn pick_wave_kernel(int win, bool roll, bool fullw, bool runner) {
+KernelFn pick_wave_kernel(int win, bool roll, bool fullw, bool runner, int L) {
   switch (win) {
-    case 0: return pick_wave_win<0>(roll, fullw, runner);
-    case 3: return pick_wave_win<3>(roll, fullw, runner);
-    case 5: return pick_wave_win<5>(roll, fullw, runner);
-    case 7: return pick_wave_win<7>(roll, fullw, runner);
+    case 0: return pick_wave_win<0>(roll, fullw, runner, L);
+    case 3: return pick_wave_win<3>(roll, fullw, runner, L);
+    case 5: return pick_wave_win<5>(roll, fullw, runner, L);
+    case 7: return pick_wave_win<7>(roll, fullw, runner, L);
   }
   return nullptr;
 }
@@ -1215,7 +1323,7 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream) {
     const bool fullw = g.N == g.L && g.E % g.EPW == 0;
     const bool runner = roll && a.reward && a.term && a.node && a.edge && a.avail &&
                         a.traj_pos && a.traj_done && a.traj_t && a.obs_window && !a.obs_full;
-    KernelFn fn = pick_wave_kernel(a.obs_window ? g.window : 0, roll, fullw, runner);
+    KernelFn fn = pick_wave_kernel(a.obs_window ? g.window : 0, roll, fullw, runner, g.L);
     if (fn) {
       const int blocks = (g.E + g.EPW - 1) / g.EPW;
       hipLaunchKernelGGL(fn, dim3(blocks), dim3(64), g.wv_lds, stream, g, a);
@@ -1367,6 +1475,7 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   g.m_wpr = magic48(g.wpr);
   g.m_W = magic48(c.W);
   g.m_W4 = magic48(std::max(1, c.W / 4));
+  g.m_pitch = magic48(pitch);
   g.bits_words = (int)(((int64_t)c.H * c.W + 31) / 32);
   g.map_stride = mapfx_map_stride(c.H, c.W);
   g.map_shared = c.map_shared ? 1 : 0;

@@ -20,6 +20,7 @@ from .maps import map_stride, pack_bits
 
 _DTYPES = {torch.int8: MAPFX_I8, torch.int32: MAPFX_I32, torch.int64: MAPFX_I64}
 OBS_MODES = {"full": MAPFX_OBS_FULL, "window": MAPFX_OBS_WINDOW, "primal": MAPFX_OBS_PRIMAL}
+_OBS_KEYS = ("term", "avail", "obs_full", "obs_window", "obs_primal", "primal_vec")
 
 
 def _stream_handle() -> int:
@@ -98,6 +99,10 @@ class MapfGridBatch:
         self.err = torch.zeros((1,), dtype=torch.int32, device=dev)
         self.obs_elem = torch.int8 if lib.mapfx_obs_elem_size(self.N) == 1 else torch.int16
         self.out = self._alloc_out(None)
+        self._out_cache = {}          # outputs selection -> Out struct over self.out
+        self._dev_index = self.device.index if self.device.index is not None \
+            else torch.cuda.current_device()
+        self._act_shape = (self.E, self.N)
         self._state = _abi.State(pos=ptr(self.pos), goal=ptr(self.goal),
                                  init_pos=ptr(self.init_pos), done=ptr(self.done), t=ptr(self.t),
                                  steps=ptr(self.steps), map_bits=ptr(self.bits))
@@ -130,6 +135,21 @@ class MapfGridBatch:
             o["traj_t"] = torch.zeros((T, E), dtype=torch.int32, device=dev)
         return o
 
+    def _own_out(self, keys):
+        """Cached Out struct over the persistent self.out buffers."""
+        k = None if keys is None else tuple(keys)
+        s = self._out_cache.get(k)
+        if s is None:
+            s = self._out_cache[k] = self._out_struct(self.out, keys=k)
+        return s
+
+    def _call(self, fn, *args):
+        """Run a C-ABI call with self.device current (no context switch when it already is)."""
+        if torch.cuda.current_device() == self._dev_index:
+            return fn(*args, torch.cuda.current_stream().cuda_stream)
+        with torch.cuda.device(self.device):
+            return fn(*args, torch.cuda.current_stream().cuda_stream)
+
     def _out_struct(self, o, keys=None):
         s = _abi.Out()
         for name, _ in _abi.Out._fields_:
@@ -160,35 +180,33 @@ class MapfGridBatch:
         m = None
         if env_mask is not None:
             m = torch.as_tensor(env_mask, device=self.device).to(torch.uint8).contiguous()
-        o = self._out_struct(self.out, keys=("term", "avail", "obs_full", "obs_window",
-                                             "obs_primal", "primal_vec"))
-        with torch.cuda.device(self.device):
-            check(lib.mapfx_reset(self._h, ctypes.byref(self._state), ptr(m), ctypes.byref(o),
-                                  _stream_handle()), "mapfx_reset")
+        o = self._own_out(_OBS_KEYS)
+        check(self._call(lib.mapfx_reset, self._h, ctypes.byref(self._state), ptr(m),
+                         ctypes.byref(o)), "mapfx_reset")
         return self.out
 
     def observe(self):
-        o = self._out_struct(self.out, keys=("term", "avail", "obs_full", "obs_window",
-                                             "obs_primal", "primal_vec"))
-        with torch.cuda.device(self.device):
-            check(lib.mapfx_observe(self._h, ctypes.byref(self._state), ctypes.byref(o),
-                                    _stream_handle()), "mapfx_observe")
+        o = self._own_out(_OBS_KEYS)
+        check(self._call(lib.mapfx_observe, self._h, ctypes.byref(self._state), ctypes.byref(o)),
+              "mapfx_observe")
         return self.out
 
     def step(self, actions, outputs=None):
         """One env step of all E envs.  actions: [E, N] int8/int32/int64 tensor.
         `outputs` optionally restricts which outputs are written (names of self.out)."""
-        a = torch.as_tensor(actions, device=self.device)
-        if a.dtype not in _DTYPES:
-            a = a.to(torch.int64)
-        a = a.contiguous()
-        if tuple(a.shape) != (self.E, self.N):
+        a = actions
+        if not (isinstance(a, torch.Tensor) and a.device == self.device and a.dtype in _DTYPES
+                and a.is_contiguous()):
+            a = torch.as_tensor(a, device=self.device)
+            if a.dtype not in _DTYPES:
+                a = a.to(torch.int64)
+            a = a.contiguous()
+        if a.shape != self._act_shape:
             raise AssertionError("actions must be [%d, %d], got %s" % (self.E, self.N,
                                                                      tuple(a.shape)))
-        o = self._out_struct(self.out, keys=outputs)
-        with torch.cuda.device(self.device):
-            check(lib.mapfx_step(self._h, ctypes.byref(self._state), ptr(a), _DTYPES[a.dtype],
-                                 ctypes.byref(o), _stream_handle()), "mapfx_step")
+        o = self._own_out(outputs)
+        check(self._call(lib.mapfx_step, self._h, ctypes.byref(self._state), a.data_ptr(),
+                         _DTYPES[a.dtype], ctypes.byref(o)), "mapfx_step")
         return self.out
 
     def rollout(self, T, actions=None, seed=0, t0=0, autoreset=False, traj=None, outputs=None):

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--T", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=8)
+    ap.add_argument("--quick", action="store_true", help="runner rollout + per-step only")
     a = ap.parse_args()
     import bench
     import mapfx
@@ -45,6 +46,8 @@ def main():
         "nothing": (),
         "all+full_obs": full + ("obs_full",),
     }
+    if a.quick:
+        variants = {"all": full, "nothing": ()}
     res = {k: [] for k in variants}
     for rnd in range(a.rounds + 1):
         for name, outs in variants.items():
@@ -59,6 +62,22 @@ def main():
                 res[name].append(ev[0].elapsed_time(ev[1]) / (a.launches * T) * 1e3)
     for name, v in res.items():
         print("%-14s us/step median %.3f  min %.3f" % (name, np.median(v), np.min(v)))
+    # per-step drop-in path: one mapfx_step launch per env step
+    pouts = ("reward", "term", "node", "edge", "avail", "obs_window")
+    ks = 100
+    for k in range(10):
+        b.step(acts[k], outputs=pouts)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(ks)]
+    for k in range(ks):
+        ev[k][0].record()
+        b.step(acts[k], outputs=pouts)
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    print("%-14s us/step median %.3f" % ("per_step", np.median([x.elapsed_time(y) * 1e3 for x, y in ev])))
+    if a.quick:
+        return
     # rng actions instead of HBM actions
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]

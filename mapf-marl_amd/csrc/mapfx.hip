@@ -587,23 +587,36 @@ __device__ unsigned long long g_stamps[256 * 8];
   } while (0)
 #endif
 
-// Padded u8 cell map of one env from its LDS bitmap, one map row per lane at a
-// time: border rows / pad words are constant, an interior word is one 4-bit
-// window of the bitmap row spread to the four cells' obstacle flags.  No
-// division and no per-word bounds tests.
-__device__ inline void build_map_rows_u8(const Geo& g, uint32_t* map32, const uint32_t* bitsL,
-                                         int lane, int nl) {
+// Wave-path cell format: one byte per padded cell, c = count + 1 - obstacle, so
+//   c == 0  <=> obstacle with no agent on it (and every border cell): the move /
+//               avail / window "obstacle" test of the reference (:278-280, :209-222,
+//               marl_partial.py:335-337) is a plain zero test;
+//   agents plane = max(count - obstacle, 0) = c - (c != 0);  occ = c - 1;
+// and adding / removing an agent is +-1 with no borrow (c >= 1 under an agent).
+// The static obstacle flag lives in bit 7 of the per-cell `dep` byte (the low 7
+// bits hold the move direction of the cell's occupant in the current step).
+// Built one map row per lane at a time: border rows / pad words are constant, an
+// interior word is one 4-bit window of the bitmap row spread over four cells.
+__device__ inline void build_map_rows_c(const Geo& g, uint32_t* map32, uint32_t* dep32,
+                                        const uint32_t* bitsL, int lane, int nl) {
   const int wpr = g.wpr, plw = g.pl >> 2;
   const int iw = (g.W + 3) >> 2;  // interior words (the last one may hold border cells)
   const uint32_t last_or = (g.W & 3) ? ((0xFu << (g.W & 3)) & 0xFu) : 0u;
   for (int pr = lane; pr < g.rows; pr += nl) {
     uint32_t* row = map32 + pr * wpr;
+    uint32_t* drow = dep32 + pr * wpr;
     const int rr = pr - g.P;
     if (rr < 0 || rr >= g.H) {
-      for (int w = 0; w < wpr; ++w) row[w] = 0x80808080u;
+      for (int w = 0; w < wpr; ++w) {
+        row[w] = 0u;
+        drow[w] = 0xFFFFFFFFu;
+      }
       continue;
     }
-    for (int w = 0; w < plw; ++w) row[w] = 0x80808080u;
+    for (int w = 0; w < plw; ++w) {
+      row[w] = 0u;
+      drow[w] = 0xFFFFFFFFu;
+    }
     // 32 cells (8 map words) per bitmap read pair: the reads of a chunk are waited
     // for once, not once per word
     for (int k0 = 0; k0 < iw; k0 += 8) {
@@ -614,11 +627,16 @@ __device__ inline void build_map_rows_u8(const Geo& g, uint32_t* map32, const ui
         if (k0 + j < iw) {
           uint32_t nib = (x >> (4 * j)) & 0xFu;
           if (k0 + j == iw - 1) nib |= last_or;
-          row[plw + k0 + j] = ((nib * 0x00204081u) & 0x01010101u) * 0x80u;
+          const uint32_t f = (nib * 0x00204081u) & 0x01010101u;  // obstacle flag per cell
+          row[plw + k0 + j] = f ^ 0x01010101u;
+          drow[plw + k0 + j] = (f << 7) | 0x7F7F7F7Fu;
         }
       }
     }
-    for (int w = plw + iw; w < wpr; ++w) row[w] = 0x80808080u;
+    for (int w = plw + iw; w < wpr; ++w) {
+      row[w] = 0u;
+      drow[w] = 0xFFFFFFFFu;
+    }
   }
 }
 
@@ -628,14 +646,12 @@ __device__ inline void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// 4 padded-map cells (one u32, bytes = obstacle flag 0x80 | count) ->
-// obstacle plane bytes (occ == -1) and agents plane bytes (max(occ, 0)).
+// 4 cells of the c format (one u32) -> obstacle plane bytes (c == 0) and agents
+// plane bytes (c - (c != 0)); c <= 127 so the +0x7F carry never leaves its byte.
 __device__ inline void swar_window(uint32_t v, uint32_t& ob, uint32_t& ag) {
-  const uint32_t f = (v >> 7) & 0x01010101u;
-  const uint32_t cnt = v & 0x7F7F7F7Fu;
-  const uint32_t nz = ((cnt + 0x7F7F7F7Fu) >> 7) & 0x01010101u;  // 1 where count >= 1
-  ob = f & (nz ^ 0x01010101u);
-  ag = cnt - (f & nz);
+  const uint32_t nz = ((v + 0x7F7F7F7Fu) >> 7) & 0x01010101u;  // 1 where c >= 1
+  ob = nz ^ 0x01010101u;
+  ag = v - nz;
 }
 
 // OR a chunk of `bits` (<= 56) bits into a little-endian u64 bit stream at `pos`
@@ -653,12 +669,15 @@ __device__ __forceinline__ void put_bits(uint64_t (&w)[NW], int pos, int bits, u
 // cols 4-7 (R[.. + WIN + y]).  Register index of record byte b and its byte lane:
 template <int WIN>
 __host__ __device__ constexpr int rec_reg(int b) {
-  return (b / (WIN * WIN)) * 2 * WIN + ((b % (WIN * WIN)) % WIN >= 4 ? WIN : 0) +
-         (b % (WIN * WIN)) / WIN;
+  const int plane = b / (WIN * WIN), y = (b % (WIN * WIN)) / WIN, x = (b % (WIN * WIN)) % WIN;
+  if (WIN == 5 && x == 4) return plane * 2 * WIN + WIN + (y < 4 ? 0 : 1);  // packed column 4
+  return plane * 2 * WIN + (x >= 4 ? WIN : 0) + y;
 }
 template <int WIN>
 __host__ __device__ constexpr int rec_lane(int b) {
-  return ((b % (WIN * WIN)) % WIN) & 3;
+  const int y = (b % (WIN * WIN)) / WIN, x = (b % (WIN * WIN)) % WIN;
+  if (WIN == 5 && x == 4) return y < 4 ? y : 0;
+  return x & 3;
 }
 // Dword k of the record (bytes 4k..4k+3) as at most two v_perm_b32 of register pairs.
 struct PermSpec {
@@ -707,8 +726,10 @@ __device__ __forceinline__ void rec_words(const uint32_t (&R)[4 * WIN], uint32_t
   ((w[K] = rec_word<WIN, K>(R)), ...);
 }
 
-// Direct HBM variant of stage_record (diagnostic comparison, MAPFX_DIRECT_REC=1):
-// same split into one u16 + dword stores, written straight to global memory.
+// One agent's 2*WIN*WIN-byte record straight to HBM.  Records are 2-byte aligned
+// (2*WIN^2 = 2 mod 4): a record at 2 mod 4 is written as one u16 then dwords
+// shifted by two bytes (one v_perm each), one at 0 mod 4 as dwords then one u16,
+// so every store is naturally aligned and no byte of a neighbour's record is touched.
 template <int WIN>
 __device__ __forceinline__ void write_record(const uint32_t (&R)[4 * WIN], unsigned char* rec) {
   constexpr int REC = 2 * WIN * WIN;
@@ -717,10 +738,10 @@ __device__ __forceinline__ void write_record(const uint32_t (&R)[4 * WIN], unsig
   uint32_t w[NW];
   rec_words<WIN>(R, w, std::make_integer_sequence<int, NW>{});
   const bool odd = (((uintptr_t)rec) & 2) != 0;
+  const uint32_t sel = odd ? 0x05040302u : 0x03020100u;  // bytes 2..5 of {w[j+1], w[j]}
   unsigned char* dbase = rec + (odd ? 2 : 0);
 #pragma unroll
-  for (int j = 0; j < ND; ++j)
-    *(uint32_t*)(dbase + 4 * j) = odd ? __builtin_amdgcn_alignbyte(w[j + 1], w[j], 2) : w[j];
+  for (int j = 0; j < ND; ++j) *(uint32_t*)(dbase + 4 * j) = __builtin_amdgcn_perm(w[j + 1], w[j], sel);
   *(uint16_t*)(rec + (odd ? 0 : REC - 2)) = (uint16_t)(odd ? w[0] : w[NW - 1]);
 }
 
@@ -841,10 +862,11 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
     for (int i = lane64; i < 2 * rew_buf; i += 64) rewL[i] = 0.0;
   }
   wave_fence();
-  build_map_rows_u8(g, map32, bitsL, ag, L);
+  build_map_rows_c(g, map32, (uint32_t*)dep, bitsL, ag, L);
   wave_fence();
   if (has) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
   wave_fence();
+  uint32_t f_cur = has ? (uint32_t)dep[cur] >> 7 : 0u;  // obstacle flag of the agent's cell
 
   const auto cell_rc = [&](int cell) {  // padded cell -> (row, col)
     const int pr = fastdiv(cell, g.m_pitch);
@@ -930,28 +952,51 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
     uint32_t R[WIN > 0 ? 4 * WIN : 1];  // [plane][cols 0-3 | cols 4-7][row]
     if constexpr (WIN > 0) {
       const int o = (q_nc - H2) & 3;  // same byte offset in every row (pitch % 4 == 0)
-      uint32_t X0[WIN], X1[WIN];
+      uint32_t X0[WIN];
 #pragma unroll
       for (int y = 0; y < WIN; ++y) {
-        X0[y] = __builtin_amdgcn_alignbyte(qx[WIN + y], qx[y], o);           // cells 0-3
-        X1[y] = __builtin_amdgcn_alignbyte(qx[2 * WIN + y], qx[WIN + y], o);  // cells 4-7
+        X0[y] = __builtin_amdgcn_alignbyte(qx[WIN + y], qx[y], o);  // cells 0-3
         swar_window(X0[y], R[y], R[2 * WIN + y]);
         R[WIN + y] = R[3 * WIN + y] = 0;
-        if (WIN > 4) swar_window(X1[y], R[WIN + y], R[3 * WIN + y]);
       }
-      const uint32_t ctr = ((H2 >= 4 ? X1[H2] : X0[H2]) >> (8 * (H2 & 3))) & 0x7Fu;
-      node = ctr > 1u ? 1u : 0u;
+      if constexpr (WIN == 5) {  // column 4 of rows 0-3 (and of row 4) in one register
+        const uint32_t o4 = (uint32_t)o * 0x0101u;
+        const uint32_t c0 = __builtin_amdgcn_perm(qx[WIN + 1], qx[WIN + 0], 0x0C0C0400u + o4) |
+                            __builtin_amdgcn_perm(qx[WIN + 3], qx[WIN + 2], 0x04000C0Cu + (o4 << 16));
+        const uint32_t c1 = __builtin_amdgcn_alignbyte(0u, qx[WIN + 4], o);
+        swar_window(c0, R[WIN + 0], R[3 * WIN + 0]);
+        swar_window(c1, R[WIN + 1], R[3 * WIN + 1]);
+      } else if constexpr (WIN > 5) {
+#pragma unroll
+        for (int y = 0; y < WIN; ++y)
+          swar_window(__builtin_amdgcn_alignbyte(qx[2 * WIN + y], qx[WIN + y], o), R[WIN + y],
+                      R[3 * WIN + y]);  // cells 4-7
+      }
+      const uint32_t ctr = (X0[H2] >> (8 * H2)) & 0xFFu;  // H2 <= 3: centre is in cells 0-3
+      node = ctr + (q_dj >> 7) >= 3u ? 1u : 0u;            // count = c - 1 + obstacle >= 2
     } else {
-      node = (qx[0] & 0x7Fu) > 1u ? 1u : 0u;
+      node = (qx[0] & 0xFFu) + (q_dj >> 7) >= 3u ? 1u : 0u;
     }
     if (q_skip) node = 0;
-    uint32_t availm = 16u;  // avail (:203-224): neighbour not (obstacle, 0 agents)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) availm |= (((q_nb >> (8 * d)) & 0xFFu) != 0x80u) ? (1u << d) : 0u;
+    // avail (:203-224): a neighbour is available iff its c != 0; stay always
+    const uint32_t nzn = ((q_nb + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
+    const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
     if constexpr (WIN > 0) {
       if (want_win && has && !(MAPFX_ABLATE & 1)) {
 #if MAPFX_DIRECT_REC
+#ifdef MAPFX_DIAG_COAL  // diagnostic only: same record words, lane-contiguous 16 B stores
+        {
+          constexpr int NW = (REC + 3) / 4;
+          uint32_t w[NW];
+          rec_words<WIN>(R, w, std::make_integer_sequence<int, NW>{});
+          uint4* d = (uint4*)((unsigned char*)a.obs_window + (size_t)(so + env0 * N) * REC) + lane64 * 3;
+          d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+          d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+          d[2] = make_uint4(w[8], w[9], w[10], w[11] ^ w[12]);
+        }
+#else
         write_record<WIN>(R, (unsigned char*)a.obs_window + (size_t)(so + oa) * REC);
+#endif
 #else
         stage_record<WIN>(R, lds + g.wv_off_stage + buf * g.wv_stage_buf +
                                  (uint32_t)(slot * N + ag) * REC);  // -> LDS staging
@@ -979,7 +1024,7 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
     int edge = 0;
     const bool suspect = q_moved && q_pre > 0;
     if (__ballot(suspect)) {
-      if (suspect && q_pre == 1) edge = q_dj == (uint32_t)(q_act ^ 1) ? 1 : 0;
+      if (suspect && q_pre == 1) edge = (q_dj & 0x7Fu) == (uint32_t)(q_act ^ 1) ? 1 : 0;
       if (__ballot(suspect && q_pre > 1)) {  // stacked pre-occupants: scan the env
         for (int j = 0; j < N; ++j) {
           const int oj2 = __shfl(q_oc, base + j);
@@ -1055,14 +1100,14 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
     // ---------------- A: move decision on the PRE-step map (:319-342) ----------------
     const int oc = cur;
     const bool mv = !dn && (uint32_t)act < 4u;  // 4 = stay, 0xFF = invalid (!has: 4)
-    const uint32_t v = mv ? ((nb >> ((act & 3) * 8)) & 0xFFu) : 0x80u;  // pre-step cell
-    const bool envc = mv && v == 0x80u;  // out of bounds / free-standing obstacle (quirk 1)
+    const uint32_t v = mv ? ((nb >> ((act & 3) * 8)) & 0xFFu) : 0u;  // pre-step cell (c)
+    const bool envc = mv && v == 0u;  // out of bounds / free-standing obstacle (quirk 1)
     const bool skip = !do_step || ((__ballot(act == 0xFF) & envmask) != 0);
-    const bool moved = mv && v != 0x80u && !skip;
+    const bool moved = mv && v != 0u && !skip;
     int dlt = (act & 2) ? 1 : pitch;  // 0: up, 1: down, 2: left, 3: right
     dlt = (act & 1) ? dlt : -dlt;
     const int nc = moved ? oc + dlt : oc;
-    if (has && !(MAPFX_ABLATE & 64)) dep[oc] = moved ? (unsigned char)act : (unsigned char)0xFF;
+    if (has && !(MAPFX_ABLATE & 64)) dep[oc] = (unsigned char)((f_cur << 7) | (moved ? (uint32_t)act : 0x7Fu));
     if (!(MAPFX_ABLATE & 16)) {
       if (FULLW) {  // branch-free: lanes that stay add 0 to their own cell's word
         atomicAdd(&map32[oc >> 2], moved ? 0u - (1u << ((oc & 3) * 8)) : 0u);
@@ -1116,6 +1161,7 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
     } else {
       nbn = (x[1] & 0xFFu) | ((x[2] & 0xFFu) << 8) | ((xl & 0xFFu) << 16) | ((xr & 0xFFu) << 24);
     }
+    f_cur = dj >> 7;  // dep[nc] bit 7: static obstacle flag of the agent's new cell
     const bool dn_old = dn;
     const bool live = !skip && !(MAPFX_ABLATE & 128);
     if (live && nc == gcell) dn = true;          // :112-114 (goal reached)
@@ -1134,15 +1180,13 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
           const int rr_ = fastdiv(i, g.m_W4);
           const int cw = i - rr_ * wpr_out;
           const uint32_t vv = map32[((rr_ + g.P) * pitch + g.pl) / 4 + cw];
-          const uint32_t f = (vv >> 7) & 0x01010101u;
-          ((uint32_t*)outb)[i] = (((vv & 0x7F7F7F7Fu) | 0x80808080u) - f) ^ 0x80808080u;
+          ((uint32_t*)outb)[i] = ((vv | 0x80808080u) - 0x01010101u) ^ 0x80808080u;  // c - 1
         }
       } else {
         for (int i = ag; i < g.H * Wd; i += L) {
           const int rr_ = fastdiv(i, g.m_W);
           const int cc_ = i - rr_ * Wd;
-          const uint32_t vv = map[(rr_ + g.P) * pitch + cc_ + g.pl];
-          ((int8_t*)outb)[i] = (int8_t)((int)(vv & 0x7Fu) - (int)(vv >> 7));
+          ((int8_t*)outb)[i] = (int8_t)((int)map[(rr_ + g.P) * pitch + cc_ + g.pl] - 1);
         }
       }
     }
@@ -1156,7 +1200,7 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
     q_oc = oc;
     q_nc = nc;
     q_act = act;
-    q_pre = (int)(v & 0x7Fu);
+    q_pre = (int)v - 1 + (int)(dj >> 7);  // pre-step occupants of cand (moved lanes)
     q_dj = dj;
     q_nb = nbn;
     q_moved = moved;
@@ -1180,9 +1224,11 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
       }
       tcur = 0;
       wave_fence();
-      if (has)
+      if (has) {
         nb = (uint32_t)map[cur - pitch] | ((uint32_t)map[cur + pitch] << 8) |
              ((uint32_t)map[cur - 1] << 16) | ((uint32_t)map[cur + 1] << 24);
+        f_cur = (uint32_t)dep[cur] >> 7;
+      }
     }
     wave_fence();
     STAMP(6);

@@ -25,7 +25,12 @@ def load_fixture(name):
 
 def step_fixtures():
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-                  if not os.path.basename(p).startswith("primal"))
+                  if not os.path.basename(p).startswith(("primal", "mp_")))
+
+
+def partial_fixtures():
+    """MARL_PARTIAL_ENV goldens (tests/golden/gen_partial_fixtures.py)."""
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "mp_*.npz")))
 
 
 def primal_fixtures():

@@ -85,6 +85,7 @@ struct Geo {
   uint64_t m_W;            // fastdiv magic for W
   uint64_t m_W4;           // fastdiv magic for W/4
   uint64_t m_pitch;        // fastdiv magic for the padded pitch (cells)
+  uint32_t m_pitch24;      // ceil(2^24 / pitch): cell -> row with one v_mul_hi_u32_u24
   int wpr;
   // LDS regions (byte offsets from the dynamic LDS base)
   int off_map, off_bits, off_oldc, off_newc, off_rc, off_goal, off_rew, off_flag, off_stage;
@@ -569,6 +570,11 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
 #ifndef MAPFX_ABLATE
 #define MAPFX_ABLATE 0  // diagnostic builds only: bit mask of parts skipped for timing
 #endif
+#ifdef MAPFX_CLOCKS
+// Diagnostic build only: per-wave shader-clock / 100 MHz real-time clock at the
+// start and end of the step loop, read back with mapfx_debug_clocks().
+__device__ unsigned long long g_clk[8 * 32768];
+#endif
 #ifdef MAPFX_STAMPS
 // Diagnostic build only (never the shipped library): per-segment s_memtime stamps
 // of block 0 / lane 0, read back with mapfx_debug_stamps().
@@ -726,23 +732,31 @@ __device__ __forceinline__ void rec_words(const uint32_t (&R)[4 * WIN], uint32_t
   ((w[K] = rec_word<WIN, K>(R)), ...);
 }
 
+// Store at a 32-bit byte offset from a uniform base: global_store with saddr
+// (every output offset of a launch is < 2^31, checked on the host).
+template <typename T>
+__device__ __forceinline__ void st_off(void* base, uint32_t off, T v) {
+  *(T*)((unsigned char*)base + off) = v;
+}
+
 // One agent's 2*WIN*WIN-byte record straight to HBM.  Records are 2-byte aligned
 // (2*WIN^2 = 2 mod 4): a record at 2 mod 4 is written as one u16 then dwords
 // shifted by two bytes (one v_perm each), one at 0 mod 4 as dwords then one u16,
 // so every store is naturally aligned and no byte of a neighbour's record is touched.
 template <int WIN>
-__device__ __forceinline__ void write_record(const uint32_t (&R)[4 * WIN], unsigned char* rec) {
+__device__ __forceinline__ void write_record(const uint32_t (&R)[4 * WIN], void* base, uint32_t off) {
   constexpr int REC = 2 * WIN * WIN;
   constexpr int NW = (REC + 3) / 4;
   constexpr int ND = (REC - 2) / 4;
   uint32_t w[NW];
   rec_words<WIN>(R, w, std::make_integer_sequence<int, NW>{});
-  const bool odd = (((uintptr_t)rec) & 2) != 0;
+  const bool odd = (off & 2) != 0;  // base is 256-byte aligned (torch allocations)
   const uint32_t sel = odd ? 0x05040302u : 0x03020100u;  // bytes 2..5 of {w[j+1], w[j]}
-  unsigned char* dbase = rec + (odd ? 2 : 0);
+  // one 64-bit base per record: the 12 dwords then merge into dwordx4 stores
+  unsigned char* d = (unsigned char*)base + (off + (odd ? 2u : 0u));
 #pragma unroll
-  for (int j = 0; j < ND; ++j) *(uint32_t*)(dbase + 4 * j) = __builtin_amdgcn_perm(w[j + 1], w[j], sel);
-  *(uint16_t*)(rec + (odd ? 0 : REC - 2)) = (uint16_t)(odd ? w[0] : w[NW - 1]);
+  for (int j = 0; j < ND; ++j) *(uint32_t*)(d + 4 * j) = __builtin_amdgcn_perm(w[j + 1], w[j], sel);
+  st_off(base, off + (odd ? 0u : (uint32_t)(REC - 2)), (uint16_t)(odd ? w[0] : w[NW - 1]));
 }
 
 // 32-bit LDS address of a pointer into dynamic shared memory
@@ -801,6 +815,9 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   constexpr int NX = WIN > 0 ? WIN : 1;
   constexpr bool FIXN = FULLW && LL > 0;   // N == LL known at compile time
   constexpr bool FLAT = RUNNER && FULLW;   // env outputs stored by every lane of the env
+#ifdef MAPFX_CLOCKS
+  const unsigned long long rtk0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int L = LL > 0 ? LL : g.L;
   const int lshift = LL > 0 ? (LL == 64 ? 6 : LL == 32 ? 5 : LL == 16 ? 4 : LL == 8 ? 3 : LL == 4 ? 2 : LL == 2 ? 1 : 0)
                             : g.lshift;
@@ -868,9 +885,10 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   wave_fence();
   uint32_t f_cur = has ? (uint32_t)dep[cur] >> 7 : 0u;  // obstacle flag of the agent's cell
 
-  const auto cell_rc = [&](int cell) {  // padded cell -> (row, col)
-    const int pr = fastdiv(cell, g.m_pitch);
-    return make_int2(pr - g.P, cell - pr * pitch - g.pl);
+  const auto cell_rc = [&](int cell) {  // padded cell -> (row, col); cell < 2^16, pitch < 256
+    const uint32_t pr = (uint32_t)(((uint64_t)(((uint32_t)cell << 8) & 0xFFFFFFu) *
+                                    (uint64_t)(g.m_pitch24 & 0xFFFFFFu)) >> 32);
+    return make_int2((int)pr - g.P, cell - (int)pr * pitch - g.pl);
   };
   // `sum(rewards)`: naive left fold in agent order (:141) over the env's LDS row
   // (padded with +0.0: adding +0.0 never changes a sum that starts at +0.0)
@@ -902,14 +920,14 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   auto tail = [&](int buf, uint32_t se_t, bool skip_t, bool alldone_t, int tcur_t, double R) {
     const uint32_t ei = se_t + env;
     if (FLAT) {  // every lane of the env stores the same values: no lane branch
-      a.reward[ei] = R;
-      a.term[ei] = alldone_t ? 1 : 0;
-      a.traj_t[ei] = tcur_t;
+      st_off(a.reward, ei * 8u, R);
+      st_off(a.term, ei, (uint8_t)(alldone_t ? 1 : 0));
+      st_off(a.traj_t, ei * 4u, tcur_t);
     } else if (env_ok && ag == 0) {
       if (RUNNER) {
-        a.reward[ei] = R;
-        a.term[ei] = alldone_t ? 1 : 0;
-        a.traj_t[ei] = tcur_t;
+        st_off(a.reward, ei * 8u, R);
+        st_off(a.term, ei, (uint8_t)(alldone_t ? 1 : 0));
+        st_off(a.traj_t, ei * 4u, tcur_t);
       } else {
         if (do_step && a.reward) a.reward[ei] = R;
         if (a.term) a.term[ei] = alldone_t ? 1 : 0;
@@ -995,7 +1013,7 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
           d[2] = make_uint4(w[8], w[9], w[10], w[11] ^ w[12]);
         }
 #else
-        write_record<WIN>(R, (unsigned char*)a.obs_window + (size_t)(so + oa) * REC);
+        write_record<WIN>(R, a.obs_window, (so + oa) * (uint32_t)REC);
 #endif
 #else
         stage_record<WIN>(R, lds + g.wv_off_stage + buf * g.wv_stage_buf +
@@ -1008,7 +1026,7 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
       const int2 rc = cell_rc(q_nc);
       if (RUNNER) {
         a.node[ai] = (uint8_t)node;
-        ((int2*)a.traj_pos)[ai] = rc;
+        st_off(a.traj_pos, ai * 8u, rc);
         a.traj_done[ai] = q_dn ? 1 : 0;
         a.avail[ai] = (uint8_t)availm;
       } else {
@@ -1061,6 +1079,10 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   if (has)
     nb = (uint32_t)map[cur - pitch] | ((uint32_t)map[cur + pitch] << 8) |
          ((uint32_t)map[cur - 1] << 16) | ((uint32_t)map[cur + 1] << 24);
+#ifdef MAPFX_CLOCKS
+  const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   for (int s = 0; s < T; ++s) {
     if ((s & (AB - 1)) == 0) {  // actions of steps s .. s+AB-1, packed 4 per u32
       int v[AB];
@@ -1233,6 +1255,19 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
     wave_fence();
     STAMP(6);
   }
+#ifdef MAPFX_CLOCKS
+  {
+    const unsigned long long clk1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+    if (lane64 == 0 && blockIdx.x < 32768) {
+      g_clk[8 * blockIdx.x + 0] = clk0;
+      g_clk[8 * blockIdx.x + 1] = clk1;
+      g_clk[8 * blockIdx.x + 2] = rt0;
+      g_clk[8 * blockIdx.x + 3] = rt1;
+      g_clk[8 * blockIdx.x + 4] = rtk0;
+    }
+  }
+#endif
   // ---- drain the pipeline: heavy part of the last step, the last two tails ----
   if (T > 0) {
     const double Rp = (ROLL && T > 1) ? fold(T & 1) : 0.0;  // step T-2's row
@@ -1249,6 +1284,10 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
     if (a.steps) a.steps[oa] = st;
   }
   if (env_ok && ag == 0) a.t[env] = tcur;
+#ifdef MAPFX_CLOCKS
+  __builtin_amdgcn_s_waitcnt(0);
+  if (lane64 == 0 && blockIdx.x < 32768) g_clk[8 * blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // One env step (mapfx_step) or an observation pass (mapfx_observe, do_step = 0).
@@ -1437,6 +1476,12 @@ extern "C" {
 
 int mapfx_abi_version(void) { return MAPFX_ABI_VERSION; }
 
+#ifdef MAPFX_CLOCKS
+extern "C" int mapfx_debug_clocks(unsigned long long* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_clk), sizeof(unsigned long long) * 8 * 32768) ==
+                 hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef MAPFX_STAMPS
 int mapfx_debug_stamps(unsigned long long* host_out) {
   return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 256 * 8) ==
@@ -1522,6 +1567,7 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   g.m_W = magic48(c.W);
   g.m_W4 = magic48(std::max(1, c.W / 4));
   g.m_pitch = magic48(pitch);
+  g.m_pitch24 = (uint32_t)(((1u << 24) + pitch - 1) / pitch);
   g.bits_words = (int)(((int64_t)c.H * c.W + 31) / 32);
   g.map_stride = mapfx_map_stride(c.H, c.W);
   g.map_shared = c.map_shared ? 1 : 0;
@@ -1599,11 +1645,11 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     g.wv_rew_buf = round_up(EPW * g.wv_rew_row * 8, 16);
     g.wv_off_rew = o;
     o += 2 * g.wv_rew_buf;
-    g.wv_stage_buf = round_up(EPW * g.stage_env_bytes, 16);
+    g.wv_stage_buf = MAPFX_DIRECT_REC ? 0 : round_up(EPW * g.stage_env_bytes, 16);
     g.wv_off_stage = o;
     o += 2 * g.wv_stage_buf;
     g.wv_lds = o;
-    g.wave_ok = (o <= 64 * 1024) ? 1 : 0;
+    g.wave_ok = (o <= 64 * 1024 && pitch < 256 && g.rows * pitch < 65536) ? 1 : 0;
   }
 
   const int lds_total = g.off_stage + EPB * g.stage_env_bytes;

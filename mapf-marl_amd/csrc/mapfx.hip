@@ -1476,6 +1476,9 @@ extern "C" {
 
 int mapfx_abi_version(void) { return MAPFX_ABI_VERSION; }
 
+// error hook for the other translation unit of the library (partial.hip)
+int mapfx_internal_error(int code, const char* msg) { return set_error(code, "%s", msg); }
+
 #ifdef MAPFX_CLOCKS
 extern "C" int mapfx_debug_clocks(unsigned long long* host_out) {
   return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_clk), sizeof(unsigned long long) * 8 * 32768) ==

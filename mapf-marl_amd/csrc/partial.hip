@@ -1,0 +1,680 @@
+// partial.hip -- MI355X (gfx950) batched MARL_PARTIAL_ENV step.
+//
+// The env the reference registers (MARL-curve-main/src/envs/__init__.py:60),
+// envs/marl_partial.py (paths below relative to it):
+//   step :165-310 -- moves against the PRE-step occupancy (obstacle passable while
+//     occupied, :508-512), move / stay / stay-at-goal / env-collision rewards, goal
+//     flags, episode limit, BFS-distance "closer" reward (:213-220), node / edge
+//     collisions, completion bonus gamma^-(limit - t) (:289-299), fp64 sum in agent
+//     order;
+//   get_obs :312-375 -- w x w obstacle / agents planes + K nearest agents x 13
+//     features (stable sort by L2 distance, self first, -1 padding), float32;
+//   get_state :377-387, avail :399-433;
+//   goal distances :906-928 -- A* path lengths == BFS levels (bit-parallel BFS).
+//
+// Layout: one wavefront holds EPW envs (L = pow2ceil(N) lanes per env, lane =
+// agent); an env's padded cell map (c = count + 1 - obstacle, c == 0 blocked /
+// border) and its dep map (bit 7: obstacle, bits 0-6: the occupant's move) live in
+// LDS for the launch; state round-trips HBM between calls.  Every fp64 value is
+// computed in the reference's operation order; sqrt(int) and the completion bonus
+// come from host-libm LUTs (math.sqrt / float ** int are correctly rounded there).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+
+#include "internal.h"
+#include "mapfx.h"
+#include "mapfx_partial.h"
+
+namespace {
+
+constexpr int NF = 13;   // KNN features per agent (:81)
+constexpr int FR = 12;   // per-agent feature row in LDS (all but the pairwise distance)
+constexpr int BONUS_EXTRA = 65536;  // completion-bonus LUT entries past the episode limit
+
+struct PGeo {
+  int H, W, N, E;
+  int L, lshift, EPW;
+  int P, pl, pitch, rows, wpr;       // padded LDS map
+  int bits_words, map_shared;
+  long long map_stride;
+  int map_env_bytes, bits_env_bytes, feat_env_bytes, rew_env_bytes;
+  int off_map, off_dep, off_bits, off_feat, off_pos, off_rew, lds;
+  int win, K, D, limit, hw;          // window, knn, obs dim, episode limit, H*W
+  double move_rew, stay_rew, stay_goal_rew, nc_rew, ec_rew, env_rew;
+  int sq_max, bonus_len;             // LUT sizes
+};
+
+struct PArgs {
+  int32_t* pos;
+  const int32_t* goal;
+  const int32_t* init_pos;
+  int32_t* steps;
+  uint8_t* at_goal;
+  uint8_t* done;
+  int32_t* goal_cost;
+  uint8_t* node;
+  int32_t* edge;
+  int32_t* t;
+  uint8_t* terminated;
+  int32_t* total_coll;
+  const uint8_t* bits;
+  const int16_t* gd;
+  const void* actions;
+  int act_dtype;
+  int do_step;       // 0: observe only
+  const uint8_t* reset_mask;  // reset pass: envs to reset (NULL = all); nullptr when not resetting
+  int do_reset;
+  double* reward;
+  float* obs;
+  float* state;
+  uint8_t* avail;
+  int32_t* err;
+  const double* sqrt_lut;   // sqrt(n), n = 0 .. sq_max
+  const double* bonus_lut;  // (complete / gamma ** (limit - t)) * fac, t = 0 .. bonus_len-1
+};
+
+__device__ inline int load_act(const void* p, int dtype, long long idx) {
+  if (dtype == MAPFX_I8) return (int)((const int8_t*)p)[idx];
+  if (dtype == MAPFX_I32) return ((const int32_t*)p)[idx];
+  const long long v = ((const int64_t*)p)[idx];
+  return (v < -1 || v > 5) ? -1 : (int)v;
+}
+
+__device__ inline void wave_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---------------------------------------------------------------------------
+// BFS distance tables: one wave per (env, agent), lane r holds row r of the grid
+// as a 64-bit mask; each level expands the frontier by shifts (same row) and
+// shuffles (rows r-1, r+1).  Distances go to LDS then out, row-major int16.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) partial_bfs_kernel(PGeo g, const uint8_t* bits,
+                                                         const int32_t* goal, const uint8_t* mask,
+                                                         int16_t* gd) {
+  __shared__ int16_t dist[64 * 64];
+  const int pair = blockIdx.x;  // env * N + agent
+  const int env = pair / g.N;
+  if (mask && !mask[env]) return;  // uniform per block
+  const int r = threadIdx.x;
+  const int H = g.H, W = g.W;
+  const uint64_t wmask = W == 64 ? ~0ull : ((1ull << W) - 1ull);
+  // free cells of row r
+  uint64_t freem = 0;
+  if (r < H) {
+    const uint8_t* b = bits + (g.map_shared ? 0 : (long long)env * g.map_stride);
+    for (int c = 0; c < W; ++c) {
+      const int idx = r * W + c;
+      if (!((b[idx >> 3] >> (idx & 7)) & 1)) freem |= 1ull << c;
+    }
+  }
+  for (int i = r; i < H * W; i += 64) dist[i] = -1;
+  wave_fence();
+  const int gr = goal[2 * pair], gc = goal[2 * pair + 1];
+  uint64_t front = (r == gr && ((freem >> gc) & 1)) ? (1ull << gc) : 0ull;
+  uint64_t seen = front;
+  if (front) dist[r * W + gc] = 0;
+  int level = 0;
+  while (__ballot(front != 0)) {
+    ++level;
+    const uint64_t up = __shfl_up(front, 1);    // row r-1
+    const uint64_t dn = __shfl_down(front, 1);  // row r+1
+    uint64_t nxt = (front << 1) | (front >> 1);
+    if (r > 0) nxt |= up;
+    if (r < 63) nxt |= dn;
+    nxt &= freem & wmask & ~seen;
+    if (r >= H) nxt = 0;
+    seen |= nxt;
+    for (uint64_t m = nxt; m; m &= m - 1) dist[r * W + __builtin_ctzll(m)] = (int16_t)level;
+    front = nxt;
+  }
+  wave_fence();
+  int16_t* out = gd + (long long)pair * g.hw;
+  for (int i = r; i < g.hw; i += 64) out[i] = dist[i];
+}
+
+// ---------------------------------------------------------------------------
+// Step / observe / reset kernel (one launch = one env step or observation pass).
+// ---------------------------------------------------------------------------
+template <int WIN>
+__global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  constexpr int H2 = WIN / 2;
+  const int lane64 = threadIdx.x;
+  const int slot = lane64 >> g.lshift;
+  const int ag = lane64 & (g.L - 1);
+  const int base = slot << g.lshift;
+  const int env = blockIdx.x * g.EPW + slot;
+  const int N = g.N;
+  const bool env_ok = slot < g.EPW && env < g.E;
+  const bool has = env_ok && ag < N;
+  const uint64_t envmask = (g.L == 64 ? ~0ull : ((1ull << g.L) - 1ull)) << base;
+  const int pitch = g.pitch;
+  const int cs = env_ok ? slot : 0;  // LDS slot (idle lanes alias slot 0, write nothing)
+
+  unsigned char* map = lds + g.off_map + cs * g.map_env_bytes;
+  uint32_t* map32 = (uint32_t*)map;
+  unsigned char* dep = lds + g.off_dep + cs * g.map_env_bytes;
+  uint32_t* dep32 = (uint32_t*)dep;
+  uint32_t* bitsL = (uint32_t*)(lds + g.off_bits + cs * g.bits_env_bytes);
+  float* feat = (float*)(lds + g.off_feat + cs * g.feat_env_bytes);
+  int2* posL = (int2*)(lds + g.off_pos + cs * (64 * 8));
+  double* rewL = (double*)(lds + g.off_rew + cs * g.rew_env_bytes);
+
+  const long long oa = (long long)env * N + ag;
+  // ---- state ----
+  int r = 0, c = 0, gr = 0, gc = 0, ir = 0, ic = 0, steps = 0, gcost = -1, edge = 0;
+  bool at_goal = false, dn = false;
+  uint32_t node = 0;
+  int tcur = 0, total = 0;
+  bool term = false;
+  bool reset_me = false;
+  if (env_ok) {
+    reset_me = a.do_reset && (!a.reset_mask || a.reset_mask[env]);
+    tcur = a.t[env];
+    term = a.terminated[env] != 0;
+    total = a.total_coll[env];
+  }
+  if (has) {
+    const int2 q = ((const int2*)a.goal)[oa];
+    const int2 ip = ((const int2*)a.init_pos)[oa];
+    gr = q.x;
+    gc = q.y;
+    ir = ip.x;
+    ic = ip.y;
+    if (reset_me) {  // :125-163
+      r = ir;
+      c = ic;
+    } else {
+      const int2 p = ((const int2*)a.pos)[oa];
+      r = p.x;
+      c = p.y;
+      steps = a.steps[oa];
+      at_goal = a.at_goal[oa] != 0;
+      dn = a.done[oa] != 0;
+      gcost = a.goal_cost[oa];
+      node = a.node[oa];
+      edge = a.edge[oa];
+    }
+  }
+  if (reset_me) {
+    tcur = 0;
+    term = false;
+    total = 0;
+  }
+  // ---- LDS map (c format) + dep map (obstacle flag in bit 7) ----
+  if (env_ok) {
+    const uint32_t* src = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)env * g.map_stride));
+    for (int w = ag; w < g.bits_words; w += g.L) bitsL[w] = src[w];
+  }
+  wave_fence();
+  if (env_ok) {
+    for (int wi = ag; wi < g.rows * g.wpr; wi += g.L) {
+      const int pr = wi / g.wpr, pw = wi - pr * g.wpr;
+      const int rr = pr - g.P;
+      uint32_t f = 0x01010101u;  // obstacle flags of the word's 4 cells
+      if (rr >= 0 && rr < g.H) {
+        f = 0;
+        for (int j = 0; j < 4; ++j) {
+          const int cc = pw * 4 + j - g.pl;
+          uint32_t ob = 1;
+          if (cc >= 0 && cc < g.W) {
+            const int idx = rr * g.W + cc;
+            ob = (bitsL[idx >> 5] >> (idx & 31)) & 1u;
+          }
+          f |= ob << (8 * j);
+        }
+      }
+      map32[wi] = f ^ 0x01010101u;  // c = 1 - obstacle before agents are added
+      dep32[wi] = (f << 7) | 0x7F7F7F7Fu;
+    }
+  }
+  wave_fence();
+  int cur = (r + g.P) * pitch + c + g.pl;
+  if (has) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
+  wave_fence();
+
+  // ---- step (:165-310) ----
+  if (a.do_step && env_ok) {
+    int act = 4;
+    if (has) {
+      act = load_act(a.actions, a.act_dtype, oa);
+      if (act < 0 || act > 4) act = -1;
+    }
+    const bool skip = (__ballot(act < 0) & envmask) != 0;  // the reference asserts (:174)
+    if (!skip) {
+      ++tcur;  // :178
+      double rew = 0.0;  // rewards[i] = 0 (:183)
+      bool moved = false;
+      int nc = cur;
+      uint32_t v = 0;
+      if (has && !dn) {  // :193-211
+        ++steps;
+        bool envc = false;
+        if (act != 4) {
+          const int d = act == 0 ? -pitch : act == 1 ? pitch : act == 2 ? -1 : 1;
+          v = map[cur + d];   // PRE-step occupancy: 0 = out of bounds / free-standing obstacle
+          if (v == 0) envc = true;
+          else {
+            nc = cur + d;
+            moved = true;
+          }
+        }
+        if (envc) rew = rew + g.env_rew;                    // :203
+        if (act != 4) rew = rew + g.move_rew;               // :207
+        else rew = rew + (at_goal ? g.stay_goal_rew : g.stay_rew);  // :209-212
+      }
+      const int nr = r + (moved ? (act == 0 ? -1 : act == 1 ? 1 : 0) : 0);
+      const int ncol = c + (moved ? (act == 2 ? -1 : act == 3 ? 1 : 0) : 0);
+      at_goal = has && nr == gr && ncol == gc;              // :214-219
+      if (at_goal) gcost = tcur;
+      if (tcur >= g.limit) {                                // :221-225
+        term = true;
+        dn = true;
+      }
+      if (has) {                                            // :227-233
+        const int16_t* gdt = a.gd + oa * g.hw;
+        const int opd = gdt[r * g.W + c];
+        const int npd = gdt[nr * g.W + ncol];
+        rew = rew + (double)(opd - npd) / (double)g.limit;
+      }
+      // counts move; node / edge collisions (:708-727, :822-857)
+      if (has) dep[cur] = (unsigned char)((dep[cur] & 0x80u) | (moved ? (uint32_t)act : 0x7Fu));
+      wave_fence();
+      if (moved) {
+        atomicSub(&map32[cur >> 2], 1u << ((cur & 3) * 8));
+        atomicAdd(&map32[nc >> 2], 1u << ((nc & 3) * 8));
+      }
+      wave_fence();
+      const uint32_t dj = has ? dep[nc] : 0x7Fu;
+      const uint32_t cn = has ? map[nc] : 0u;
+      node = (has && cn + (dj >> 7) >= 3u) ? 1u : 0u;
+      const int pre = (int)v - 1 + (int)(dj >> 7);
+      edge = 0;
+      const bool suspect = moved && pre > 0;
+      if (__ballot(suspect)) {
+        if (suspect && pre == 1) edge = (dj & 0x7Fu) == (uint32_t)(act ^ 1) ? 1 : 0;
+        if (__ballot(suspect && pre > 1)) {
+          for (int j = 0; j < N; ++j) {
+            const int oj = __shfl(cur, base + j);
+            const int nj = __shfl(nc, base + j);
+            if (suspect && pre > 1) edge += (oj == nc) & (nj == cur);
+          }
+        }
+      }
+      // env sums: total collisions += (sum(node) + sum(edge)) // 2  (:239)
+      int esum = has ? (int)node + edge : 0;
+      for (int o = 1; o < g.L; o <<= 1) esum += __shfl_xor(esum, o);
+      total += esum / 2;
+      rew = rew + g.nc_rew * (double)node;  // :247
+      rew = rew + g.ec_rew * (double)edge;  // :249
+      r = nr;
+      c = ncol;
+      cur = nc;
+      // all at goals: dones, terminated, completion bonus (:283-299)
+      const bool all_at = (__ballot(has && !at_goal) & envmask) == 0;
+      if (all_at) {
+        dn = true;
+        term = true;
+        const int bi = min(tcur, g.bonus_len - 1);
+        rew = rew + a.bonus_lut[bi];
+      }
+      // sum(rewards): naive left fold in agent order (:310)
+      if (has) rewL[ag] = rew;
+      wave_fence();
+      if (ag == 0) {
+        double R = 0.0;
+        for (int j = 0; j < N; ++j) R = R + rewL[j];
+        if (a.reward) a.reward[env] = R;
+      }
+    } else {
+      if (ag == 0 && a.err) atomicCAS(a.err, 0, env + 1);
+      if (ag == 0 && a.reward) a.reward[env] = 0.0;
+    }
+  }
+  wave_fence();
+
+  // ---- observations of the current state (:312-391) ----
+  // per-agent feature rows: curr, start, goal, unit vec, norm, node, edge, steps
+  if (has) {
+    const int d0 = gr - r, d1 = gc - c;
+    const double nrm = a.sqrt_lut[d0 * d0 + d1 * d1];        // :937
+    const double ux = nrm == 0.0 ? 0.0 : (double)d0 / nrm;   // :938-941
+    const double uy = nrm == 0.0 ? 0.0 : (double)d1 / nrm;
+    float* fr = feat + ag * FR;
+    fr[0] = (float)r; fr[1] = (float)c; fr[2] = (float)ir; fr[3] = (float)ic;
+    fr[4] = (float)gr; fr[5] = (float)gc; fr[6] = (float)ux; fr[7] = (float)uy;
+    fr[8] = (float)nrm; fr[9] = (float)node; fr[10] = (float)edge; fr[11] = (float)steps;
+    posL[ag] = make_int2(r, c);
+  }
+  wave_fence();
+  if (has && a.obs) {
+    float* o = a.obs + oa * g.D;
+    // window planes (:327-342): OOB / obstacle -> 1; agents -> count
+    if constexpr (WIN > 0) {
+      for (int y = 0; y < WIN; ++y) {
+        for (int x = 0; x < WIN; ++x) {
+          const uint32_t cv = map[cur + (y - H2) * pitch + (x - H2)];
+          o[y * WIN + x] = cv == 0 ? 1.0f : 0.0f;
+          o[WIN * WIN + y * WIN + x] = cv == 0 ? 0.0f : (float)(cv - 1u);  // max(count - obst, 0)
+        }
+      }
+    }
+    // K nearest agents (:346-372): self first, then the k-1 nearest others by L2
+    // distance (sorted() is stable: ties by agent index); rows past min(N, K) = -1
+    float* kn = o + 2 * WIN * WIN;
+    const int K = g.K;
+    const int km1 = min(N, K) - 1;
+    for (int q = 0; q < 13; ++q) kn[q] = feat[ag * FR + (q < 11 ? q : 11)];
+    kn[11] = (float)(g.H * g.W);  // distance to itself (:543-545)
+    kn[12] = feat[ag * FR + 11];
+    long long prev = -1;
+    for (int s = 1; s <= km1; ++s) {
+      long long best = 0x7FFFFFFFFFFFFFFFll;
+      for (int j = 0; j < N; ++j) {
+        if (j == ag) continue;
+        const int2 pj = posL[j];
+        const int dr = r - pj.x, dc = c - pj.y;
+        const long long key = (long long)(dr * dr + dc * dc) * 64 + j;
+        if (key > prev && key < best) best = key;
+      }
+      prev = best;
+      const int j = (int)(best & 63);
+      const int sq = (int)(best >> 6);
+      float* row = kn + s * NF;
+      for (int q = 0; q < 11; ++q) row[q] = feat[j * FR + q];
+      row[11] = (float)a.sqrt_lut[sq];
+      row[12] = feat[j * FR + 11];
+    }
+    for (int s = km1 + 1; s < K; ++s)
+      for (int q = 0; q < NF; ++q) kn[s * NF + q] = -1.0f;
+  }
+  // avail (:399-433): neighbour in bounds and not a free-standing obstacle
+  if (has && a.avail) {
+    uint32_t m = 16u;
+    if (map[cur - pitch]) m |= 1u;
+    if (map[cur + pitch]) m |= 2u;
+    if (map[cur - 1]) m |= 4u;
+    if (map[cur + 1]) m |= 8u;
+    a.avail[oa] = (uint8_t)m;
+  }
+  // state (:377-387): [total collisions, step count, sum(each goal cost)]
+  int gsum = has ? gcost : 0;
+  for (int o = 1; o < g.L; o <<= 1) gsum += __shfl_xor(gsum, o);
+  if (env_ok && ag == 0 && a.state) {
+    a.state[3 * env + 0] = (float)total;
+    a.state[3 * env + 1] = (float)tcur;
+    a.state[3 * env + 2] = (float)gsum;
+  }
+  // ---- state write-back ----
+  if (has) {
+    ((int2*)a.pos)[oa] = make_int2(r, c);
+    a.steps[oa] = steps;
+    a.at_goal[oa] = at_goal ? 1 : 0;
+    a.done[oa] = dn ? 1 : 0;
+    a.goal_cost[oa] = gcost;
+    a.node[oa] = (uint8_t)node;
+    a.edge[oa] = edge;
+  }
+  if (env_ok && ag == 0) {
+    a.t[env] = tcur;
+    a.terminated[env] = term ? 1 : 0;
+    a.total_coll[env] = total;
+  }
+}
+
+int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+struct mapfx_partial_t {
+  mapfx_partial_cfg cfg;
+  PGeo geo;
+  double* sqrt_lut;
+  double* bonus_lut;
+  int device;
+};
+
+namespace {
+
+int perr(int code, const char* msg) { return mapfx_internal_error(code, msg); }
+
+int check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    char buf[256];
+    snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
+    return perr(MAPFX_EHIP, buf);
+  }
+  return MAPFX_OK;
+}
+
+int check_state(const mapfx_partial_t* h, const mapfx_partial_state* st) {
+  if (!st) return perr(MAPFX_EINVAL, "NULL state");
+  if (!st->pos || !st->goal || !st->init_pos || !st->steps || !st->at_goal || !st->done ||
+      !st->goal_cost || !st->node || !st->edge || !st->t || !st->terminated || !st->total_coll ||
+      !st->map_bits || !st->goal_dist)
+    return perr(MAPFX_EINVAL, "mapfx_partial_state: every pointer is required");
+  (void)h;
+  return MAPFX_OK;
+}
+
+int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
+  const PGeo& g = h->geo;
+  if (g.E == 0) return MAPFX_OK;
+  a.sqrt_lut = h->sqrt_lut;
+  a.bonus_lut = h->bonus_lut;
+  const int blocks = (g.E + g.EPW - 1) / g.EPW;
+  void (*fn)(PGeo, PArgs) = nullptr;
+  switch (g.win) {
+    case 0: fn = partial_kernel<0>; break;
+    case 1: fn = partial_kernel<1>; break;
+    case 3: fn = partial_kernel<3>; break;
+    case 5: fn = partial_kernel<5>; break;
+    case 7: fn = partial_kernel<7>; break;
+    case 9: fn = partial_kernel<9>; break;
+    default: return perr(MAPFX_EINVAL, "obs_window must be one of 0, 1, 3, 5, 7, 9");
+  }
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64), g.lds, (hipStream_t)stream, g, a);
+  return check_hip(hipGetLastError(), "partial_kernel launch");
+}
+
+void fill_state(PArgs& a, const mapfx_partial_state* st) {
+  a.pos = st->pos;
+  a.goal = st->goal;
+  a.init_pos = st->init_pos;
+  a.steps = st->steps;
+  a.at_goal = st->at_goal;
+  a.done = st->done;
+  a.goal_cost = st->goal_cost;
+  a.node = st->node;
+  a.edge = st->edge;
+  a.t = st->t;
+  a.terminated = st->terminated;
+  a.total_coll = st->total_coll;
+  a.bits = st->map_bits;
+  a.gd = st->goal_dist;
+}
+
+void fill_out(PArgs& a, const mapfx_partial_out* o) {
+  if (!o) return;
+  a.reward = o->reward;
+  a.obs = o->obs;
+  a.state = o->state;
+  a.avail = o->avail;
+  a.err = o->err;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
+  if (!cfg || !out) return perr(MAPFX_EINVAL, "NULL argument");
+  *out = nullptr;
+  const mapfx_partial_cfg& c = *cfg;
+  if (c.H < 1 || c.W < 1 || c.H > 64 || c.W > 64)
+    return perr(MAPFX_EINVAL, "MARL_PARTIAL path supports 1 <= H, W <= 64");
+  if (c.n_agents < 1 || c.n_agents > 64) return perr(MAPFX_EINVAL, "n_agents must be in 1..64");
+  if (c.n_envs < 0) return perr(MAPFX_EINVAL, "n_envs < 0");
+  if (c.episode_limit < 1) return perr(MAPFX_EINVAL, "episode_limit must be >= 1");
+  if (c.obs_knn_agents < 1) return perr(MAPFX_EINVAL, "obs_knn_agents must be >= 1");
+  if (c.obs_window < 0 || c.obs_window > 9 || (c.obs_window > 0 && !(c.obs_window & 1)))
+    return perr(MAPFX_EINVAL, "obs_window must be 0 or odd <= 9");
+  mapfx_partial_t* h = new (std::nothrow) mapfx_partial_t();
+  if (!h) return perr(MAPFX_ENOMEM, "host allocation failed");
+  h->cfg = c;
+  h->sqrt_lut = nullptr;
+  h->bonus_lut = nullptr;
+  if (hipGetDevice(&h->device) != hipSuccess) h->device = 0;
+  PGeo& g = h->geo;
+  memset(&g, 0, sizeof(g));
+  g.H = c.H;
+  g.W = c.W;
+  g.N = c.n_agents;
+  g.E = c.n_envs;
+  int L = 1;
+  while (L < g.N) L <<= 1;
+  g.L = L;
+  while ((1 << g.lshift) < L) ++g.lshift;
+  g.win = c.obs_window;
+  g.K = c.obs_knn_agents;
+  g.D = 2 * c.obs_window * c.obs_window + NF * c.obs_knn_agents;
+  g.limit = c.episode_limit;
+  g.hw = c.H * c.W;
+  g.P = std::max(1, c.obs_window / 2);
+  g.pl = round_up(g.P, 4);
+  g.pitch = round_up(g.pl + c.W + g.P, 4);
+  g.rows = c.H + 2 * g.P;
+  g.wpr = g.pitch / 4;
+  g.bits_words = (c.H * c.W + 31) / 32;
+  g.map_shared = c.map_shared ? 1 : 0;
+  g.map_stride = mapfx_map_stride(c.H, c.W);
+  g.map_env_bytes = round_up(g.rows * g.pitch, 16);
+  g.bits_env_bytes = round_up(g.bits_words * 4 + 4, 16);
+  g.feat_env_bytes = round_up(64 * FR * 4, 16);
+  g.rew_env_bytes = 64 * 8;
+  g.move_rew = c.move_reward;
+  g.stay_rew = c.stay_reward;
+  g.stay_goal_rew = c.stay_goal_reward;
+  g.nc_rew = c.node_collide_reward;
+  g.ec_rew = c.edge_collide_reward;
+  g.env_rew = c.env_collide_reward;
+  const int per_env = 2 * g.map_env_bytes + g.bits_env_bytes + g.feat_env_bytes + 64 * 8 + g.rew_env_bytes;
+  int EPW = 64 / L;
+  while (EPW > 1 && EPW * per_env > 64 * 1024) --EPW;
+  g.EPW = EPW;
+  int off = 0;
+  g.off_map = off; off += EPW * g.map_env_bytes;
+  g.off_dep = off; off += EPW * g.map_env_bytes;
+  g.off_bits = off; off += EPW * g.bits_env_bytes;
+  g.off_feat = off; off += EPW * g.feat_env_bytes;
+  g.off_pos = off; off += EPW * 64 * 8;
+  g.off_rew = off; off += EPW * g.rew_env_bytes;
+  g.lds = off;
+  // LUTs from the host libm (math.sqrt, float ** int): correctly rounded references
+  const int S = std::max(c.H, c.W);
+  g.sq_max = 2 * (S - 1) * (S - 1);
+  g.bonus_len = c.episode_limit + BONUS_EXTRA;
+  double* sq = (double*)malloc(sizeof(double) * (g.sq_max + 1));
+  double* bo = (double*)malloc(sizeof(double) * g.bonus_len);
+  if (!sq || !bo) {
+    free(sq);
+    free(bo);
+    delete h;
+    return perr(MAPFX_ENOMEM, "host allocation failed");
+  }
+  double (*volatile libm_sqrt)(double) = sqrt;
+  double (*volatile libm_pow)(double, double) = pow;
+  for (int i = 0; i <= g.sq_max; ++i) sq[i] = libm_sqrt((double)i);
+  for (int t = 0; t < g.bonus_len; ++t)  // (complete / (gamma ** (limit - t))) * fac  (:292)
+    bo[t] = (c.complete_reward / libm_pow(c.gamma, (double)(c.episode_limit - t))) * c.complete_fac;
+  int rc = check_hip(hipMalloc(&h->sqrt_lut, sizeof(double) * (g.sq_max + 1)), "hipMalloc");
+  if (!rc) rc = check_hip(hipMalloc(&h->bonus_lut, sizeof(double) * g.bonus_len), "hipMalloc");
+  if (!rc) rc = check_hip(hipMemcpy(h->sqrt_lut, sq, sizeof(double) * (g.sq_max + 1), hipMemcpyHostToDevice), "hipMemcpy");
+  if (!rc) rc = check_hip(hipMemcpy(h->bonus_lut, bo, sizeof(double) * g.bonus_len, hipMemcpyHostToDevice), "hipMemcpy");
+  free(sq);
+  free(bo);
+  if (rc) {
+    mapfx_partial_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return MAPFX_OK;
+}
+
+void mapfx_partial_destroy(mapfx_partial_t* h) {
+  if (!h) return;
+  if (h->sqrt_lut) (void)hipFree(h->sqrt_lut);
+  if (h->bonus_lut) (void)hipFree(h->bonus_lut);
+  delete h;
+}
+
+int32_t mapfx_partial_obs_dim(const mapfx_partial_t* h) { return h ? h->geo.D : -1; }
+
+int mapfx_partial_goal_dist(mapfx_partial_t* h, const mapfx_partial_state* st,
+                            const uint8_t* env_mask, void* stream) {
+  if (!h) return perr(MAPFX_EINVAL, "NULL handle");
+  int rc = check_state(h, st);
+  if (rc) return rc;
+  const PGeo& g = h->geo;
+  if ((long long)g.E * g.N == 0) return MAPFX_OK;
+  hipLaunchKernelGGL(partial_bfs_kernel, dim3(g.E * g.N), dim3(64), 0, (hipStream_t)stream, g,
+                     st->map_bits, st->goal, env_mask, st->goal_dist);
+  return check_hip(hipGetLastError(), "partial_bfs_kernel launch");
+}
+
+int mapfx_partial_reset(mapfx_partial_t* h, const mapfx_partial_state* st, const uint8_t* env_mask,
+                        const mapfx_partial_out* out, void* stream) {
+  if (!h) return perr(MAPFX_EINVAL, "NULL handle");
+  int rc = check_state(h, st);
+  if (rc) return rc;
+  PArgs a;
+  memset(&a, 0, sizeof(a));
+  fill_state(a, st);
+  fill_out(a, out);
+  a.reward = nullptr;
+  a.do_reset = 1;
+  a.reset_mask = env_mask;
+  return launch(h, a, stream);
+}
+
+int mapfx_partial_step(mapfx_partial_t* h, const mapfx_partial_state* st, const void* actions,
+                       int action_dtype, const mapfx_partial_out* out, void* stream) {
+  if (!h) return perr(MAPFX_EINVAL, "NULL handle");
+  int rc = check_state(h, st);
+  if (rc) return rc;
+  if (!actions) return perr(MAPFX_EINVAL, "NULL actions");
+  if (action_dtype < MAPFX_I8 || action_dtype > MAPFX_I64) return perr(MAPFX_EINVAL, "bad action_dtype");
+  PArgs a;
+  memset(&a, 0, sizeof(a));
+  fill_state(a, st);
+  fill_out(a, out);
+  a.actions = actions;
+  a.act_dtype = action_dtype;
+  a.do_step = 1;
+  return launch(h, a, stream);
+}
+
+int mapfx_partial_observe(mapfx_partial_t* h, const mapfx_partial_state* st,
+                          const mapfx_partial_out* out, void* stream) {
+  if (!h) return perr(MAPFX_EINVAL, "NULL handle");
+  int rc = check_state(h, st);
+  if (rc) return rc;
+  PArgs a;
+  memset(&a, 0, sizeof(a));
+  fill_state(a, st);
+  fill_out(a, out);
+  a.reward = nullptr;
+  return launch(h, a, stream);
+}
+
+}  // extern "C"

@@ -6,5 +6,6 @@ there is no CPU fallback.
 from . import rng, maps  # noqa: F401  (pure host utilities)
 from ._abi import lib, MapfxError  # noqa: F401  (fails loudly if the library is missing)
 from .batch import MapfGridBatch  # noqa: F401
+from .partial import MarlPartialBatch  # noqa: F401
 
-__all__ = ["MapfGridBatch", "MapfxError", "lib", "rng", "maps"]
+__all__ = ["MapfGridBatch", "MarlPartialBatch", "MapfxError", "lib", "rng", "maps"]

@@ -50,10 +50,34 @@ class Info(ctypes.Structure):
                 ("pad", c_i32)]
 
 
-# every symbol include/mapfx.h declares (checked by tests/test_abi_exports.py)
+class PCfg(ctypes.Structure):  # include/mapfx_partial.h
+    _fields_ = [("H", c_i32), ("W", c_i32), ("n_agents", c_i32), ("n_envs", c_i32),
+                ("env_offset", c_i64), ("episode_limit", c_i32), ("obs_window", c_i32),
+                ("obs_knn_agents", c_i32), ("map_shared", c_i32), ("move_reward", c_f64),
+                ("stay_reward", c_f64), ("stay_goal_reward", c_f64),
+                ("node_collide_reward", c_f64), ("edge_collide_reward", c_f64),
+                ("env_collide_reward", c_f64), ("complete_reward", c_f64),
+                ("complete_fac", c_f64), ("gamma", c_f64)]
+
+
+class PState(ctypes.Structure):
+    _fields_ = [(k, c_vp) for k in ("pos", "goal", "init_pos", "steps", "at_goal", "done",
+                                    "goal_cost", "node", "edge", "t", "terminated", "total_coll",
+                                    "map_bits", "goal_dist")]
+
+
+class POut(ctypes.Structure):
+    _fields_ = [(k, c_vp) for k in ("reward", "obs", "state", "avail", "err")]
+
+
+# every symbol include/mapfx.h and include/mapfx_partial.h declare
+# (checked by tests/test_abi_exports.py)
 EXPORTS = ("mapfx_abi_version", "mapfx_last_error", "mapfx_map_stride", "mapfx_obs_elem_size",
            "mapfx_create", "mapfx_destroy", "mapfx_query", "mapfx_reset", "mapfx_step",
-           "mapfx_observe", "mapfx_rollout", "mapfx_gen_actions", "mapfx_action")
+           "mapfx_observe", "mapfx_rollout", "mapfx_gen_actions", "mapfx_action",
+           "mapfx_partial_create", "mapfx_partial_destroy", "mapfx_partial_obs_dim",
+           "mapfx_partial_goal_dist", "mapfx_partial_reset", "mapfx_partial_step",
+           "mapfx_partial_observe")
 
 
 class MapfxError(RuntimeError):
@@ -81,6 +105,13 @@ def _load():
                                   c_vp]),
         "mapfx_gen_actions": (c_i32, [c_vp, c_u64, c_i32, c_i32, c_vp, c_vp]),
         "mapfx_action": (c_i32, [c_u64, c_i64, c_i32, c_i32]),
+        "mapfx_partial_create": (c_i32, [P(PCfg), P(c_vp)]),
+        "mapfx_partial_destroy": (None, [c_vp]),
+        "mapfx_partial_obs_dim": (c_i32, [c_vp]),
+        "mapfx_partial_goal_dist": (c_i32, [c_vp, P(PState), c_vp, c_vp]),
+        "mapfx_partial_reset": (c_i32, [c_vp, P(PState), c_vp, P(POut), c_vp]),
+        "mapfx_partial_step": (c_i32, [c_vp, P(PState), c_vp, c_i32, P(POut), c_vp]),
+        "mapfx_partial_observe": (c_i32, [c_vp, P(PState), P(POut), c_vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -1,0 +1,187 @@
+"""MARL_PARTIAL_ENV drop-in: the env the reference registers (src/envs/__init__.py:60).
+
+Same constructor, plugin methods, return types and RNG draw order as
+MARL-curve-main/src/envs/marl_partial.py (`MARL_PARTIAL_ENV`, lines 23-1000); the
+goal-distance tables, transition, rewards, collisions, observations, state and
+available actions come from the HIP kernels (mapfx.partial.MarlPartialBatch,
+E = 1).  Observations are float32, the dtype PyMARL's EpisodeBatch stores them
+in.  Not reproduced (out of scope): rendering / visual json export and the
+`output=True` random collision repair (:262-275).
+"""
+from __future__ import annotations
+
+import os.path
+import random
+
+import numpy as np
+import torch
+
+from ..maps import load_map
+from ..partial import MarlPartialBatch
+from .multiagentenv import MultiAgentEnv
+
+ACTION_MEANING = {0: "LEFT", 1: "RIGHT", 2: "UP", 3: "DOWN", 4: "STAY"}  # :1076-1082
+
+
+class MARL_PARTIAL_ENV(MultiAgentEnv):
+    """MultiAgentEnv, the base of customized envs"""
+
+    def __init__(self, grid_file_path, agents_path, n_agents=4, obs_window=5, obs_knn_agents=5,
+                 episode_limit=100, seed=None, render='human', move_reward=-0.01, stay_reward=-0.02,
+                 stay_goal_reward=0, node_collide_reward=-1, edge_collide_reward=-1,
+                 env_collide_reward=-1, complete_reward=1000, complete_fac=1.5, debug=False,
+                 visual=False, gamma=0.99, output=False, device=None):
+        assert os.path.exists(grid_file_path)                                    # :54
+        if output:
+            raise NotImplementedError("output mode (random collision repair, :262-275) is not "
+                                      "part of the MI355X path")
+        self._grid_file_path = grid_file_path
+        self._agent_path = agents_path
+        self._render_mode = render
+        self._debug_mode = debug
+        self._n_agents = n_agents
+        self._seed = random.randint(0, 9999)                                     # :61
+        np.random.seed(self._seed)
+        if seed:
+            self._seed = seed
+        self.agents = [a for a in range(self._n_agents)]
+        self._n_features = 13
+        self._actions = [0, 1, 2, 3, 4]
+        self.episode_limit = episode_limit
+        self._obs_window = obs_window
+        self._obs_knn_agents = obs_knn_agents
+        self._params = dict(obs_window=obs_window, obs_knn_agents=obs_knn_agents,
+                            episode_limit=episode_limit, move_reward=move_reward,
+                            stay_reward=stay_reward, stay_goal_reward=stay_goal_reward,
+                            node_collide_reward=node_collide_reward,
+                            edge_collide_reward=edge_collide_reward,
+                            env_collide_reward=env_collide_reward, complete_reward=complete_reward,
+                            complete_fac=complete_fac, gamma=gamma)
+        self._device = device
+        self._agent_init_pos = [(-1, -1) for _ in self.agents]
+        self._agent_goal_pos = [(-1, -1) for _ in self.agents]
+        self.__setup_grid()                                                      # :107
+        self.__setup_agent()                                                     # :108
+        self._batch = None
+        self._step_count = None
+        self._terminated = False
+
+    # ---------------------------------------------------------------- setup
+    def __setup_grid(self):
+        """:862-894 (map only; the networkx graph is replaced by the BFS kernel)."""
+        grid = load_map(self._grid_file_path)
+        n_rows, n_cols = grid.shape
+        assert n_rows > 0 and n_cols > 0
+        if n_rows != n_cols:  # __create_grid indexes [col][row] (:514-522): square maps only
+            raise IndexError("list index out of range")
+        self._grid_shape = (n_rows, n_cols)
+        self._grid = grid
+
+    def __setup_agent(self):
+        """:896-920: same draws (random.randint(1, 25), random.sample), scen
+        fields 4..7 = start x(col), start y(row), goal x, goal y."""
+        random_scen_path = self._agent_path + str(random.randint(1, 25)) + '.scen'
+        assert os.path.exists(random_scen_path)
+        with open(random_scen_path, "r") as f:
+            f_lines = [row.rstrip() for row in f.readlines()][1:]
+            assert len(f_lines) > self._n_agents
+            rand_lines = random.sample(f_lines, self._n_agents)
+            for a_index, f_line in enumerate(rand_lines):
+                line_list = f_line.replace('\t', ',').split(",")
+                s_col, s_row, f_col, f_row = (int(line_list[4]), int(line_list[5]),
+                                              int(line_list[6]), int(line_list[7]))
+                self._agent_init_pos[a_index] = (s_row, s_col)
+                self._agent_goal_pos[a_index] = (f_row, f_col)
+
+    def _load_instance(self):
+        init = np.array([self._agent_init_pos], dtype=np.int32)
+        goals = np.array([self._agent_goal_pos], dtype=np.int32)
+        if self._batch is None:
+            self._batch = MarlPartialBatch(init, goals, grids=self._grid[None],
+                                           device=self._device, **self._params)
+        else:
+            self._batch.set_agents(init, goals)
+
+    # ---------------------------------------------------------------- plugin API
+    def reset(self):
+        """:125-163: re-samples the agents, resets, returns get_obs()."""
+        self.__setup_agent()
+        self._load_instance()
+        self._batch.reset()
+        self._step_count = 0
+        self._terminated = False
+        self._pull()
+        return self.get_obs()
+
+    def _pull(self):
+        o = self._batch.out
+        self._obs = o["obs"][0].cpu().numpy()
+        self._state = o["state"][0].cpu().numpy()
+        self._avail_mask = o["avail"][0].cpu().numpy()
+        self._agent_positions = [tuple(int(v) for v in p) for p in self._batch.pos[0].cpu().numpy()]
+
+    def agent_pos(self, agent_id):
+        assert -1 < agent_id < self._n_agents
+        return self._agent_positions[agent_id]
+
+    def step(self, agents_action):
+        """:165-310 -- returns (sum(rewards), terminated, {'_step_count': t})."""
+        if isinstance(agents_action, torch.Tensor):
+            agents_action = agents_action.detach().cpu().numpy()
+        assert len(agents_action) == self._n_agents                              # :173
+        assert all([action_i in ACTION_MEANING.keys() for action_i in agents_action])  # :174
+        acts = torch.as_tensor(np.asarray([int(a) for a in agents_action], dtype=np.int8)[None])
+        b = self._batch
+        b.step(acts)
+        R = float(b.out["reward"][0].item())
+        self._step_count += 1
+        self._terminated = bool(b.terminated[0].item())
+        self._pull()
+        return R, self._terminated, {'_step_count': self._step_count}
+
+    def get_obs(self):
+        """:312-317 -- (N, 2W^2 + 13K), float32 values."""
+        return self._obs.copy()
+
+    def get_obs_agent(self, agent_id):
+        return self._obs[agent_id].copy()
+
+    def get_obs_size(self):
+        return 2 * (self._obs_window ** 2) + self._obs_knn_agents * self._n_features
+
+    def get_state(self):
+        """:377-387 -- [total collisions, step count, sum(each goal cost)]."""
+        return self._state.astype(np.int64)
+
+    def get_state_size(self):
+        return 3
+
+    def get_avail_actions(self):
+        return [self.get_avail_agent_actions(i) for i in self.agents]
+
+    def get_avail_agent_actions(self, agent_id):
+        m = int(self._avail_mask[agent_id])
+        return [(m >> d) & 1 for d in range(5)]
+
+    def get_total_actions(self):
+        return len(self._actions)
+
+    def render(self):
+        return None
+
+    def close(self):
+        pass
+
+    def seed(self):
+        pass
+
+    def save_replay(self):
+        pass
+
+    def get_env_info(self):
+        return {"state_shape": self.get_state_size(), "obs_shape": self.get_obs_size(),
+                "n_actions": self.get_total_actions(), "n_agents": self._n_agents,
+                "episode_limit": self.episode_limit}
+
+    def episode_done(self):
+        return bool(self._batch.done[0].all().item())

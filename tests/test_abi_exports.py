@@ -8,12 +8,15 @@ import numpy as np
 
 from conftest import REPO
 
-HEADER = os.path.join(REPO, "include", "mapfx.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("mapfx.h", "mapfx_partial.h")]
 
 
 def _declared():
-    text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:[A-Za-z_][\w\s\*]*?)\b(mapfx_\w+)\s*\(", text, re.M)))
+    out = set()
+    for hdr in HEADERS:
+        text = open(hdr).read()
+        out |= set(re.findall(r"^\s*(?:[A-Za-z_][\w\s\*]*?)\b(mapfx_\w+)\s*\(", text, re.M))
+    return sorted(out)
 
 
 def test_library_exports_every_declared_symbol():

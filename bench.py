@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--gather", action="store_true",
                     help="also time the RCCL gather of (obs, reward, done) to rank 0")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_c2.json"))
+    ap.add_argument("--env", default="mapf_grid", choices=("mapf_grid", "marl_partial"),
+                    help="mapf_grid: the BASELINE.json metric (default); marl_partial: the "
+                         "SURVEY §8(f) F1 env on its yaml config, one launch per step")
+    ap.add_argument("--partial-envs", type=int, default=4096)
     return ap.parse_args()
 
 
@@ -89,6 +93,8 @@ def main():
     import mapfx
     from mapfx.maps import synthetic_instances, warehouse_grid
 
+    if args.env == "marl_partial":
+        return run_partial(args, dist, rank, world, local)
     S, N, E, p, shared = CONFIGS[args.config]
     W = args.window
     K, WU, T = args.steps, args.warmup, args.chunk
@@ -257,6 +263,121 @@ def time_gather(dist, b, acts, outs, T, WU, K, world, E, N):
     return {"value": round(world * E * N * K / el, 1), "ms_per_step": round(el / K * 1e3, 5),
             "bytes_per_rank_per_chunk": int(og.bytes_per_chunk()), "chunk_steps": T,
             "collective": "torch.distributed.gather (RCCL) to rank 0 on a side stream"}
+
+
+PARTIAL_YAML = dict(  # MARL-curve-main/src/config/envs/marl_partial.yaml:3-23
+    obs_window=5, obs_knn_agents=5, episode_limit=100, move_reward=0, stay_reward=-0.1,
+    stay_goal_reward=1, node_collide_reward=-2000, edge_collide_reward=-2000,
+    env_collide_reward=-2000, complete_reward=1000, complete_fac=1.5, gamma=0.99)
+
+
+def partial_bytes_per_env_step(N, D, HW):
+    """Algorithmic HBM bytes of one MARL_PARTIAL env step (state round-trips HBM):
+    reads actions N + state 23N + 13 + goal/init 16N + 2 goal-distance reads 4N +
+    bitmap HW/8; writes obs 4DN + reward 8 + state 12 + avail N + state 23N + 9."""
+    return (N + 23 * N + 13 + 16 * N + 4 * N + HW // 8) + (4 * D * N + 8 + 12 + N + 23 * N + 9)
+
+
+def run_partial(args, dist, rank, world, local):
+    """MARL_PARTIAL_ENV on the reference's yaml config: 8x8 empty
+    map, 15 agents, window 5, K = 5, episode limit 100; E envs per GPU, one
+    mapfx_partial_step launch per env step, every env reset each 100 steps."""
+    import mapfx
+    from mapfx.maps import synthetic_instances
+    S, N, E = 8, 15, args.partial_envs
+    K, WU = args.steps, args.warmup
+    offset = rank * E
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.0, seed=1, env_offset=offset)
+    grids = np.zeros((1, S, S), dtype=np.int8)
+    b = mapfx.MarlPartialBatch(inst["init_pos"], inst["goals"], grids=grids,
+                               device="cuda:%d" % local, env_offset=offset, **PARTIAL_YAML)
+    b.reset()
+    limit = PARTIAL_YAML["episode_limit"]
+    ga = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                             obs=(), device="cuda:%d" % local, env_offset=offset,
+                             track_steps=False)
+    acts = ga.gen_actions(WU + K, seed=2)  # uniform actions from the device generator, in HBM
+    del ga
+    stream = torch.cuda.current_stream()
+
+    def one(k):
+        if k % limit == 0 and k:
+            b.reset()
+        b.step(acts[k])
+
+    for k in range(WU):
+        one(k)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(K)]
+    t0 = time.perf_counter()
+    for i in range(K):
+        ev[i][0].record(stream)
+        one(WU + i)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kern_ms = float(np.median([a.elapsed_time(c) for a, c in ev]))
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    D = b.obs_dim
+    bpes = partial_bytes_per_env_step(N, D, S * S)
+    achieved = E * bpes / (kern_ms * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = partial_cpu_baseline(inst, S, N, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "MARL_PARTIAL env-steps/sec (agents x envs), yaml config 8x8/15 agents",
+            "value": round(E * world * N * K / elapsed, 1), "unit": "agent-steps/s",
+            "n_gpus": world, "steps": K, "warmup": WU, "ms_per_step": round(elapsed / K * 1e3, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32+f64+f32",
+            "data": "synthetic (empty 8x8 map, distinct random starts/goals, uniform random "
+                    "actions in HBM)",
+            "config": {"workload": "marl_partial yaml: 8x8 empty, 15 agents, window 5, K 5, "
+                                   "limit 100, %d envs/GPU, one launch per step" % E,
+                       "envs_total": E * world, "agents": N, "obs_dim": D,
+                       "parallelism": "env-shard x%d" % world},
+            "env_steps_per_s": round(E * world * K / elapsed, 1),
+            "kernel_ms_per_step": round(kern_ms, 5),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "bytes_per_env_step": bpes},
+            "cpu_baseline": cpu}), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def partial_cpu_baseline(inst, S, N, seconds):
+    """The Python restatement (oracle/partial_oracle.py, the reference's algorithm
+    in plain Python, one core) on a bounded sample: as many env-steps of the same
+    workload as fit in ~`seconds`."""
+    from oracle.partial_oracle import PartialEnvState
+    grid = np.zeros((S, S), dtype=np.int8)
+    rng = np.random.default_rng(3)
+    n_done, t0 = 0, time.perf_counter()
+    e = 0
+    while time.perf_counter() - t0 < seconds:
+        env = PartialEnvState(grid, inst["init_pos"][e], inst["goals"][e], **PARTIAL_YAML)
+        for _ in range(PARTIAL_YAML["episode_limit"]):
+            env.step(rng.integers(0, 5, size=N))
+            env.obs()
+            env.avail()
+            n_done += 1
+        e += 1
+    el = time.perf_counter() - t0
+    return {"value": round(n_done * N / el, 1), "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "sample": "%d env-steps (%d episodes of 100) of the same workload: "
+                      "oracle/partial_oracle.py step + get_obs + avail, %.1f s" % (n_done, e, el)}
 
 
 def cpu_baseline(inst, S, N, E, W, seconds):

@@ -145,7 +145,8 @@ __global__ void __launch_bounds__(64) partial_bfs_kernel(PGeo g, const uint8_t* 
 // ---------------------------------------------------------------------------
 // Step / observe / reset kernel (one launch = one env step or observation pass).
 // ---------------------------------------------------------------------------
-template <int WIN>
+// KF / LF: K and lanes-per-env fixed at compile time (0: run-time generic path)
+template <int WIN, int KF, int LF>
 __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   extern __shared__ __align__(16) unsigned char lds[];
   constexpr int H2 = WIN / 2;
@@ -358,45 +359,118 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   }
   wave_fence();
   if (has && a.obs) {
-    float* o = a.obs + oa * g.D;
-    // window planes (:327-342): OOB / obstacle -> 1; agents -> count
-    if constexpr (WIN > 0) {
-      for (int y = 0; y < WIN; ++y) {
-        for (int x = 0; x < WIN; ++x) {
-          const uint32_t cv = map[cur + (y - H2) * pitch + (x - H2)];
-          o[y * WIN + x] = cv == 0 ? 1.0f : 0.0f;
-          o[WIN * WIN + y * WIN + x] = cv == 0 ? 0.0f : (float)(cv - 1u);  // max(count - obst, 0)
+    float* kn;
+    constexpr int WW = WIN * WIN;
+    if constexpr (KF > 0 && LF > 0) {
+      // -------- fast path: the whole row in registers, merged dwordx4 stores --------
+      constexpr int D = 2 * WW + NF * KF;
+      float o[D];
+      if constexpr (WIN > 0) {  // window planes (:327-342) from whole map words
+        const int wb = (cur - H2 * pitch - H2);
+        const int sh = (wb & 3) * 8;
+#pragma unroll
+        for (int y = 0; y < WIN; ++y) {
+          const uint32_t* rowp = map32 + ((wb + y * pitch) >> 2);
+          const uint64_t lo = ((uint64_t)rowp[1] << 32) | rowp[0];
+          const uint32_t x03 = (uint32_t)(lo >> sh);
+          uint32_t x47 = 0u;  // cells 4-7 (WIN > 4)
+          if constexpr (WIN > 4) {
+            const uint64_t hi = ((uint64_t)rowp[2] << 32) | rowp[1];
+            x47 = (uint32_t)(hi >> sh);
+          }
+#pragma unroll
+          for (int x = 0; x < WIN; ++x) {
+            const uint32_t cv = ((x < 4 ? x03 : x47) >> (8 * (x & 3))) & 0xFFu;
+            o[y * WIN + x] = cv == 0 ? 1.0f : 0.0f;
+            o[WW + y * WIN + x] = cv == 0 ? 0.0f : (float)(cv - 1u);  // max(count - obst, 0)
+          }
         }
       }
-    }
-    // K nearest agents (:346-372): self first, then the k-1 nearest others by L2
-    // distance (sorted() is stable: ties by agent index); rows past min(N, K) = -1
-    float* kn = o + 2 * WIN * WIN;
-    const int K = g.K;
-    const int km1 = min(N, K) - 1;
-    for (int q = 0; q < 13; ++q) kn[q] = feat[ag * FR + (q < 11 ? q : 11)];
-    kn[11] = (float)(g.H * g.W);  // distance to itself (:543-545)
-    kn[12] = feat[ag * FR + 11];
-    long long prev = -1;
-    for (int s = 1; s <= km1; ++s) {
-      long long best = 0x7FFFFFFFFFFFFFFFll;
-      for (int j = 0; j < N; ++j) {
-        if (j == ag) continue;
+      // K nearest (:346-372): keys = sq distance * 64 + index, selected by repeated min
+      uint32_t key[LF];
+#pragma unroll
+      for (int j = 0; j < LF; ++j) {
         const int2 pj = posL[j];
         const int dr = r - pj.x, dc = c - pj.y;
-        const long long key = (long long)(dr * dr + dc * dc) * 64 + j;
-        if (key > prev && key < best) best = key;
+        key[j] = (j < N && j != ag) ? (uint32_t)(dr * dr + dc * dc) * 64u + (uint32_t)j : 0xFFFFFFFFu;
       }
-      prev = best;
-      const int j = (int)(best & 63);
-      const int sq = (int)(best >> 6);
-      float* row = kn + s * NF;
-      for (int q = 0; q < 11; ++q) row[q] = feat[j * FR + q];
-      row[11] = (float)a.sqrt_lut[sq];
-      row[12] = feat[j * FR + 11];
+      const int km1 = min(N, KF) - 1;
+      float* k0 = o + 2 * WW;
+      const float* me = feat + ag * FR;
+#pragma unroll
+      for (int q = 0; q < 11; ++q) k0[q] = me[q];
+      k0[11] = (float)(g.H * g.W);  // distance to itself (:543-545)
+      k0[12] = me[11];
+      uint32_t prev = 0u;
+      bool first = true;
+#pragma unroll
+      for (int sI = 1; sI < KF; ++sI) {
+        float* row = o + 2 * WW + sI * NF;
+        if (sI <= km1) {
+          uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+          for (int j = 0; j < LF; ++j) {
+            const uint32_t kj = key[j];
+            best = (kj < best && (first || kj > prev)) ? kj : best;
+          }
+          first = false;
+          prev = best;
+          const int j = (int)(best & 63u);
+          const float* fj = feat + j * FR;
+#pragma unroll
+          for (int q = 0; q < 11; ++q) row[q] = fj[q];
+          row[11] = (float)a.sqrt_lut[best >> 6];
+          row[12] = fj[11];
+        } else {
+#pragma unroll
+          for (int q = 0; q < NF; ++q) row[q] = -1.0f;
+        }
+      }
+      uint32_t* d = (uint32_t*)(a.obs + oa * D);
+#pragma unroll
+      for (int i = 0; i < D; ++i) d[i] = __float_as_uint(o[i]);
+    } else {
+      // -------- generic path --------
+      float* o = a.obs + oa * g.D;
+      if constexpr (WIN > 0) {  // window planes (:327-342): OOB / obstacle -> 1; agents -> count
+        for (int y = 0; y < WIN; ++y) {
+          for (int x = 0; x < WIN; ++x) {
+            const uint32_t cv = map[cur + (y - H2) * pitch + (x - H2)];
+            o[y * WIN + x] = cv == 0 ? 1.0f : 0.0f;
+            o[WW + y * WIN + x] = cv == 0 ? 0.0f : (float)(cv - 1u);
+          }
+        }
+      }
+      // K nearest agents (:346-372): self first, then the k-1 nearest others by L2
+      // distance (sorted() is stable: ties by agent index); rows past min(N, K) = -1
+      kn = o + 2 * WW;
+      const int K = g.K;
+      const int km1 = min(N, K) - 1;
+      for (int q = 0; q < 11; ++q) kn[q] = feat[ag * FR + q];
+      kn[11] = (float)(g.H * g.W);  // distance to itself (:543-545)
+      kn[12] = feat[ag * FR + 11];
+      long long prev = -1;
+      for (int sI = 1; sI <= km1; ++sI) {
+        long long best = 0x7FFFFFFFFFFFFFFFll;
+        for (int j = 0; j < N; ++j) {
+          if (j == ag) continue;
+          const int2 pj = posL[j];
+          const int dr = r - pj.x, dc = c - pj.y;
+          const long long key = (long long)(dr * dr + dc * dc) * 64 + j;
+          if (key > prev && key < best) best = key;
+        }
+        prev = best;
+        const int j = (int)(best & 63);
+        const int sq = (int)(best >> 6);
+        float* row = kn + sI * NF;
+        for (int q = 0; q < 11; ++q) row[q] = feat[j * FR + q];
+        row[11] = (float)a.sqrt_lut[sq];
+        row[12] = feat[j * FR + 11];
+      }
+      for (int sI = km1 + 1; sI < K; ++sI)
+        for (int q = 0; q < NF; ++q) kn[sI * NF + q] = -1.0f;
     }
-    for (int s = km1 + 1; s < K; ++s)
-      for (int q = 0; q < NF; ++q) kn[s * NF + q] = -1.0f;
+    (void)kn;
   }
   // avail (:399-433): neighbour in bounds and not a free-standing obstacle
   if (has && a.avail) {
@@ -474,15 +548,20 @@ int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
   a.bonus_lut = h->bonus_lut;
   const int blocks = (g.E + g.EPW - 1) / g.EPW;
   void (*fn)(PGeo, PArgs) = nullptr;
-  switch (g.win) {
-    case 0: fn = partial_kernel<0>; break;
-    case 1: fn = partial_kernel<1>; break;
-    case 3: fn = partial_kernel<3>; break;
-    case 5: fn = partial_kernel<5>; break;
-    case 7: fn = partial_kernel<7>; break;
-    case 9: fn = partial_kernel<9>; break;
-    default: return perr(MAPFX_EINVAL, "obs_window must be one of 0, 1, 3, 5, 7, 9");
-  }
+  if (g.K == 5 && g.win == 5 && g.L == 16) fn = partial_kernel<5, 5, 16>;
+  else if (g.K == 5 && g.win == 5 && g.L == 8) fn = partial_kernel<5, 5, 8>;
+  else if (g.K == 5 && g.win == 5 && g.L == 32) fn = partial_kernel<5, 5, 32>;
+  else if (g.K == 5 && g.win == 3 && g.L == 16) fn = partial_kernel<3, 5, 16>;
+  else if (g.K == 5 && g.win == 7 && g.L == 16) fn = partial_kernel<7, 5, 16>;
+  else switch (g.win) {
+      case 0: fn = partial_kernel<0, 0, 0>; break;
+      case 1: fn = partial_kernel<1, 0, 0>; break;
+      case 3: fn = partial_kernel<3, 0, 0>; break;
+      case 5: fn = partial_kernel<5, 0, 0>; break;
+      case 7: fn = partial_kernel<7, 0, 0>; break;
+      case 9: fn = partial_kernel<9, 0, 0>; break;
+      default: return perr(MAPFX_EINVAL, "obs_window must be one of 0, 1, 3, 5, 7, 9");
+    }
   hipLaunchKernelGGL(fn, dim3(blocks), dim3(64), g.lds, (hipStream_t)stream, g, a);
   return check_hip(hipGetLastError(), "partial_kernel launch");
 }
@@ -568,9 +647,14 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.nc_rew = c.node_collide_reward;
   g.ec_rew = c.edge_collide_reward;
   g.env_rew = c.env_collide_reward;
-  const int per_env = 2 * g.map_env_bytes + g.bits_env_bytes + g.feat_env_bytes + 64 * 8 + g.rew_env_bytes;
+  const int per_env = 2 * g.map_env_bytes + g.bits_env_bytes + g.feat_env_bytes + 64 * 8 +
+                      g.rew_env_bytes;
   int EPW = 64 / L;
   while (EPW > 1 && EPW * per_env > 64 * 1024) --EPW;
+  if (EPW * per_env > 64 * 1024) {
+    delete h;
+    return perr(MAPFX_EINVAL, "configuration needs more than 64 KB of LDS per env (N * obs dim)");
+  }
   g.EPW = EPW;
   int off = 0;
   g.off_map = off; off += EPW * g.map_env_bytes;

@@ -154,7 +154,10 @@ def main():
     launch_bytes = E * T * bpes + state_io
     achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
 
-    # ---- per-step drop-in path (one mapfx_step launch per env step) ----
+    # ---- per-step path (one mapfx_step launch per env step) ----
+    # `ks` launches captured once as a HIP graph and replayed: kernels back to back,
+    # no Python / ctypes launch overhead between them ("eager" = one Python call
+    # per step, as the drop-in env does it, reported beside it).
     per_step = None
     if args.per_step_steps > 0:
         b2 = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
@@ -163,24 +166,41 @@ def main():
         b2.reset()
         ks = args.per_step_steps
         pouts = ("reward", "term", "node", "edge", "avail", "obs_window")
-        for k in range(min(20, ks)):
-            b2.step(acts[k], outputs=pouts)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for k in range(ks):
+                b2.step(acts[k % (WU + K)], outputs=pouts)
+        torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        pev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(ks)]
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for k in range(ks):
+                b2.step(acts[k % (WU + K)], outputs=pouts)
+        graph.replay()
+        torch.cuda.synchronize()
+        pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 3
         t1 = time.perf_counter()
-        for k in range(ks):
-            pev[k][0].record(stream)
-            b2.step(acts[k % (WU + K)], outputs=pouts)
-            pev[k][1].record(stream)
+        pe0.record(stream)
+        for _ in range(reps):
+            graph.replay()
+        pe1.record(stream)
         torch.cuda.synchronize()
         pel = time.perf_counter() - t1
-        pk_ms = float(np.mean([a.elapsed_time(c) for a, c in pev]))
+        pk_ms = pe0.elapsed_time(pe1) / (reps * ks)
+        t2 = time.perf_counter()
+        for k in range(ks):
+            b2.step(acts[k % (WU + K)], outputs=pouts)
+        torch.cuda.synchronize()
+        eager_ms = (time.perf_counter() - t2) / ks * 1e3
         cb = canonical_bytes_per_env_step(S, S, N, W)
         per_step = {
-            "value": round(E * N * ks / pel * world, 1),
-            "ms_per_step": round(pel / ks * 1e3, 5),
+            "value": round(E * N * reps * ks / pel * world, 1),
+            "ms_per_step": round(pel / (reps * ks) * 1e3, 5),
             "kernel_ms": round(pk_ms, 5),
+            "eager_ms_per_step": round(eager_ms, 5),
+            "launch": "HIP graph of %d mapfx_step launches, replayed" % ks,
             "roofline": {"bound": "hbm", "achieved": round(E * cb / (pk_ms * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(E * cb / (pk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -300,34 +320,55 @@ def run_partial(args, dist, rank, world, local):
     del ga
     stream = torch.cuda.current_stream()
 
-    def one(k):
-        if k % limit == 0 and k:
-            b.reset()
-        b.step(acts[k])
-
-    for k in range(WU):
-        one(k)
+    # One episode (reset + `limit` steps, one kernel launch each) captured once as a
+    # HIP graph and replayed: the per-step launches run back to back without the
+    # Python / ctypes launch overhead of the drop-in path between them.
+    if K % limit or WU % limit:
+        raise SystemExit("--steps and --warmup must be multiples of the episode limit (%d)" % limit)
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        b.reset()
+        for k in range(limit):           # eager warm-up of every launch before capture
+            b.step(acts[k])
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(graph):
+        b.reset()
+        for k in range(limit):
+            b.step(acts[k])
+    for _ in range(WU // limit):
+        graph.replay()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(K)]
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for i in range(K):
-        ev[i][0].record(stream)
-        one(WU + i)
-        ev[i][1].record(stream)
+    e0.record(stream)
+    for _ in range(K // limit):
+        graph.replay()
+    e1.record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    kern_ms = float(np.median([a.elapsed_time(c) for a, c in ev]))
+    kern_ms = e0.elapsed_time(e1) / K   # per env step, including the per-episode reset
     el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    # the drop-in style (one Python call per step) for reference
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    b.reset()
+    for k in range(limit):
+        b.step(acts[k])
+    torch.cuda.synchronize()
+    eager_ms = (time.perf_counter() - t1) / limit * 1e3
     D = b.obs_dim
     bpes = partial_bytes_per_env_step(N, D, S * S)
     achieved = E * bpes / (kern_ms * 1e-3) / 1e9
@@ -340,14 +381,16 @@ def run_partial(args, dist, rank, world, local):
             "value": round(E * world * N * K / elapsed, 1), "unit": "agent-steps/s",
             "n_gpus": world, "steps": K, "warmup": WU, "ms_per_step": round(elapsed / K * 1e3, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32+f64+f32",
-            "data": "synthetic (empty 8x8 map, distinct random starts/goals, uniform random "
-                    "actions in HBM)",
+            "data": "synthetic (empty 8x8 map, distinct random starts/goals; one episode of "
+                    "uniform random actions in HBM, replayed every episode)",
             "config": {"workload": "marl_partial yaml: 8x8 empty, 15 agents, window 5, K 5, "
-                                   "limit 100, %d envs/GPU, one launch per step" % E,
+                                   "limit 100, %d envs/GPU, one launch per step, episodes "
+                                   "replayed as a HIP graph (reset + 100 steps)" % E,
                        "envs_total": E * world, "agents": N, "obs_dim": D,
                        "parallelism": "env-shard x%d" % world},
             "env_steps_per_s": round(E * world * K / elapsed, 1),
             "kernel_ms_per_step": round(kern_ms, 5),
+            "eager_ms_per_step": round(eager_ms, 5),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None, "bytes_per_env_step": bpes},

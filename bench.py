@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--gather", action="store_true",
                     help="also time the RCCL gather of (obs, reward, done) to rank 0")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_c2.json"))
-    ap.add_argument("--env", default="mapf_grid", choices=("mapf_grid", "marl_partial"),
+    ap.add_argument("--env", default="mapf_grid", choices=("mapf_grid", "marl_partial", "runner"),
                     help="mapf_grid: the BASELINE.json metric (default); marl_partial: the "
                          "SURVEY §8(f) F1 env on its yaml config, one launch per step")
     ap.add_argument("--partial-envs", type=int, default=4096)
@@ -95,6 +95,8 @@ def main():
 
     if args.env == "marl_partial":
         return run_partial(args, dist, rank, world, local)
+    if args.env == "runner":
+        return run_runner(args, dist, rank, world, local)
     S, N, E, p, shared = CONFIGS[args.config]
     W = args.window
     K, WU, T = args.steps, args.warmup, args.chunk
@@ -397,6 +399,96 @@ def run_partial(args, dist, rank, world, local):
             "cpu_baseline": cpu}), flush=True)
     if dist:
         dist.barrier()
+        dist.destroy_process_group()
+
+
+class RandomAvailMAC:
+    """select_actions: uniform over each agent's available actions, on the device
+    (the shape of epsilon-greedy at epsilon = 1, action_selectors.py:65-69)."""
+
+    def __init__(self, seed=0):
+        self.gen = None
+        self.seed = seed
+
+    def init_hidden(self, batch_size):
+        pass
+
+    def select_actions(self, batch, t_ep, t_env, bs, test_mode=False):
+        idx = torch.as_tensor(bs, dtype=torch.long, device=batch.device)
+        avail = batch["avail_actions"][idx, t_ep].float()
+        if self.gen is None:
+            self.gen = torch.Generator(device=avail.device)
+            self.gen.manual_seed(self.seed)
+        n = avail.shape[0] * avail.shape[1]
+        if n == 0:
+            return torch.zeros(avail.shape[:2], dtype=torch.long, device=avail.device)
+        return torch.multinomial(avail.view(n, -1), 1, generator=self.gen).view(avail.shape[:2])
+
+
+def run_runner(args, dist, rank, world, local):
+    """the batched ParallelRunner (mapfx/runners.py) collecting
+    episodes of the marl_partial yaml config into device-resident EpisodeBatch
+    storage, a random-available-action MAC choosing actions from the batch."""
+    import tempfile
+    import types
+    from mapfx.episode import DeviceEpisodeBatch
+    from mapfx.maps import synthetic_instances
+    from mapfx.runners import ParallelRunner
+    S, N, B = 8, 15, args.partial_envs
+    inst = synthetic_instances(B, S, S, N, p_obstacle=0.0, seed=1, env_offset=rank * B)
+    tmp = tempfile.mkdtemp(prefix="mapfx_runner_")
+    mp = os.path.join(tmp, "empty-8-8.map")
+    with open(mp, "w") as f:
+        f.write("type octile\nheight 8\nwidth 8\nmap\n" + "\n".join(["." * 8] * 8) + "\n")
+    ea = dict(PARTIAL_YAML, grid_file_path=mp, agents_path=os.path.join(tmp, "x-"), n_agents=N)
+    rargs = types.SimpleNamespace(env="marl_partial", batch_size_run=B, device="cuda:%d" % local,
+                                  env_args=ea, episode_batch_cls=DeviceEpisodeBatch,
+                                  test_nepisode=B, runner_log_interval=1 << 62)
+    runner = ParallelRunner(rargs, None, instance_fn=lambda e: (inst["init_pos"][e], inst["goals"][e]))
+    info = runner.get_env_info()
+    scheme = {"state": {"vshape": info["state_shape"]},
+              "obs": {"vshape": info["obs_shape"], "group": "agents"},
+              "actions": {"vshape": (1,), "group": "agents", "dtype": torch.long},
+              "avail_actions": {"vshape": (info["n_actions"],), "group": "agents",
+                                "dtype": torch.int},
+              "reward": {"vshape": (1,)}, "terminated": {"vshape": (1,), "dtype": torch.uint8}}
+    runner.setup(scheme, {"agents": N}, None, RandomAvailMAC(seed=rank))
+    runs = max(1, args.steps // info["episode_limit"])
+    for _ in range(max(1, args.warmup // info["episode_limit"])):
+        runner.run()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t_env0 = runner.t_env
+    t0 = time.perf_counter()
+    for _ in range(runs):
+        runner.run()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    steps = runner.t_env - t_env0
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.barrier()
+    elapsed = float(el.item())
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = partial_cpu_baseline(inst, S, N, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "ParallelRunner env-steps/sec (agents x envs) into EpisodeBatch, marl_partial yaml",
+            "value": round(steps * world * N / elapsed, 1), "unit": "agent-steps/s", "n_gpus": world,
+            "steps": runs * info["episode_limit"], "warmup": args.warmup,
+            "ms_per_step": round(elapsed / max(1, runs * info["episode_limit"]) * 1e3, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32+f64+f32",
+            "data": "synthetic (empty 8x8 map, distinct random starts/goals, random available actions "
+                    "chosen on the device from the batch)",
+            "config": {"workload": "batched ParallelRunner.run(): %d envs x 100-step episodes, "
+                                   "mapfx.episode.DeviceEpisodeBatch storage" % B,
+                       "envs_total": B * world, "agents": N, "parallelism": "env-shard x%d" % world},
+            "env_steps_per_s": round(steps * world / elapsed, 1),
+            "cpu_baseline": cpu}), flush=True)
+    if dist:
         dist.destroy_process_group()
 
 

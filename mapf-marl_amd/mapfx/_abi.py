@@ -70,14 +70,28 @@ class POut(ctypes.Structure):
     _fields_ = [(k, c_vp) for k in ("reward", "obs", "state", "avail", "err")]
 
 
-# every symbol include/mapfx.h and include/mapfx_partial.h declare
+class QCfg(ctypes.Structure):  # include/mapfx_primal.h
+    _fields_ = [(k, c_i32) for k in ("H", "W", "n_agents", "n_envs", "obs_size", "map_shared")]
+
+
+class QState(ctypes.Structure):
+    _fields_ = [(k, c_vp) for k in ("pos", "goal", "map_bits")]
+
+
+class QOut(ctypes.Structure):
+    _fields_ = [(k, c_vp) for k in ("reward", "done", "next_mask", "on_goal", "valid", "obs", "vec",
+                                    "err")]
+
+
+# every symbol include/mapfx.h, include/mapfx_partial.h and include/mapfx_primal.h declare
 # (checked by tests/test_abi_exports.py)
 EXPORTS = ("mapfx_abi_version", "mapfx_last_error", "mapfx_map_stride", "mapfx_obs_elem_size",
            "mapfx_create", "mapfx_destroy", "mapfx_query", "mapfx_reset", "mapfx_step",
            "mapfx_observe", "mapfx_rollout", "mapfx_gen_actions", "mapfx_action",
            "mapfx_partial_create", "mapfx_partial_destroy", "mapfx_partial_obs_dim",
            "mapfx_partial_goal_dist", "mapfx_partial_reset", "mapfx_partial_step",
-           "mapfx_partial_observe")
+           "mapfx_partial_observe", "mapfx_primal_create", "mapfx_primal_destroy",
+           "mapfx_primal_act")
 
 
 class MapfxError(RuntimeError):
@@ -112,6 +126,9 @@ def _load():
         "mapfx_partial_reset": (c_i32, [c_vp, P(PState), c_vp, P(POut), c_vp]),
         "mapfx_partial_step": (c_i32, [c_vp, P(PState), c_vp, c_i32, P(POut), c_vp]),
         "mapfx_partial_observe": (c_i32, [c_vp, P(PState), P(POut), c_vp]),
+        "mapfx_primal_create": (c_i32, [P(QCfg), P(c_vp)]),
+        "mapfx_primal_destroy": (None, [c_vp]),
+        "mapfx_primal_act": (c_i32, [c_vp, P(QState), c_vp, c_vp, c_i32, P(QOut), c_vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

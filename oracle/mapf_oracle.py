@@ -209,13 +209,14 @@ def window_obs(occ: np.ndarray, pos, window: int = 5) -> np.ndarray:
     return out
 
 
-def primal_obs(grid: np.ndarray, pos, goals, size: int = 10):
+def primal_obs(grid: np.ndarray, pos, goals, size: int = 10, agents=None):
     """PRIMAL `_observe`, envs/mapf_primal.py:343-386, applied to a MAPF_GRID
     state.  PRIMAL's world holds one agent id per cell (an agent overrides the
     obstacle it stands on); with stacked agents every agent on a cell counts as
     visible.  Parity with the reference is pinned on distinct positions/goals.
 
-    Returns maps (N, 4, s, s) uint8 [poss, goal, goals, obs] and vec (N, 3) f64.
+    Returns maps (N, 4, s, s) uint8 [poss, goal, goals, obs] and vec (N, 3) f64;
+    with `agents` (a list of indices) only those rows are filled.
     """
     n = len(pos)
     # Python ints, as PRIMAL's State holds them (mapf_primal.py:53-66): numpy
@@ -229,7 +230,7 @@ def primal_obs(grid: np.ndarray, pos, goals, size: int = 10):
     maps = np.zeros((n, 4, size, size), dtype=np.uint8)
     vec = np.zeros((n, 3), dtype=np.float64)
     half = size // 2
-    for a in range(n):
+    for a in (range(n) if agents is None else agents):
         pr, pc = pos[a]
         tr, tc = pr - half, pc - half
         visible = []

@@ -1,0 +1,157 @@
+"""GPU parity of batched PRIMAL sequential dynamics through the
+C ABI (include/mapfx_primal.h): against the reference's own outputs
+(tests/golden/pd_*.npz) and against the CPU restatement (oracle/primal_dyn_oracle.py)
+on batched random worlds.  Everything bit-exact: rewards and goal vectors as fp64
+bit patterns, observation maps, masks, flags and positions exactly."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+FIXTURES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "pd_*.npz")))
+
+
+@pytest.fixture(scope="module")
+def mapfx_mod():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mapfx
+    return mapfx
+
+
+def _load(name):
+    with np.load(os.path.join(GOLDEN, name + ".npz")) as z:
+        return {k: z[k] for k in z.files}
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("chunk", [0, 1, 7])
+def test_primal_matches_reference_goldens(mapfx_mod, name, chunk):
+    """All calls in one launch (chunk 0) or split over launches of `chunk` calls:
+    the world state carries over between launches."""
+    fx = _load(name)
+    b = mapfx_mod.PrimalBatch(fx["starts"][None], fx["goals"][None], grids=fx["grid"][None],
+                              observation_size=int(fx["size"]))
+    n = len(fx["agent"])
+    step = n if chunk == 0 else chunk
+    for k0 in range(0, n, step):
+        k1 = min(n, k0 + step)
+        o = b.act(fx["agent"][None, k0:k1], fx["action"][None, k0:k1])
+        sl = slice(k0, k1)
+        assert np.array_equal(_np(o["reward"])[0].view(np.uint64), fx["reward"][sl].view(np.uint64))
+        assert np.array_equal(_np(o["done"])[0].astype(bool), fx["done"][sl])
+        assert np.array_equal(_np(o["next_mask"])[0], fx["next_mask"][sl])
+        assert np.array_equal(_np(o["on_goal"])[0].astype(bool), fx["on_goal"][sl])
+        assert np.array_equal(_np(o["valid"])[0].astype(bool), fx["valid"][sl])
+        assert np.array_equal(_np(o["obs"])[0], fx["obs"][sl])
+        assert np.array_equal(_np(o["vec"])[0].view(np.uint64), fx["vec"][sl].view(np.uint64))
+        assert np.array_equal(_np(b.pos)[0], fx["pos"][k1 - 1])
+    b.check_err()
+
+
+def test_primal_dropin_matches_reference_goldens(mapfx_mod):
+    from mapfx.primal import MAPFEnv
+    fx = _load("pd_script5")
+    world = fx["grid"].astype(np.int64)
+    gg = np.zeros_like(world)
+    for a, ((r, c), (gr, gc)) in enumerate(zip(fx["starts"], fx["goals"])):
+        world[r, c] = a + 1
+        gg[gr, gc] = a + 1
+    env = MAPFEnv(num_agents=len(fx["starts"]), observation_size=int(fx["size"]), world0=world,
+                  goals0=gg)
+    for k in range(len(fx["agent"])):
+        (maps, vec), r, done, nxt, on_goal, blocking, valid = env._step(
+            (int(fx["agent"][k]), int(fx["action"][k])))
+        assert np.float64(r).view(np.uint64) == fx["reward"][k].view(np.uint64)
+        assert done == bool(fx["done"][k]) and on_goal == bool(fx["on_goal"][k])
+        assert valid == bool(fx["valid"][k]) and blocking is False
+        assert sum(1 << a for a in nxt) == int(fx["next_mask"][k])
+        assert np.array_equal(np.stack(maps), fx["obs"][k])
+        assert np.array_equal(np.array(vec).view(np.uint64), fx["vec"][k].view(np.uint64))
+        assert env.getPositions() == [tuple(p) for p in fx["pos"][k].tolist()]
+    assert env.finished == bool(fx["done"].any())
+
+
+def _random_worlds(rng, E, H, W, N, density, shared):
+    n_maps = 1 if shared else E
+    grids = np.where(rng.random((n_maps, H, W)) < density, -1, 0).astype(np.int8)
+    starts = np.zeros((E, N, 2), np.int32)
+    goals = np.zeros((E, N, 2), np.int32)
+    for e in range(E):
+        free = np.argwhere(grids[0 if shared else e] == 0)
+        idx = rng.choice(len(free), size=2 * N, replace=False)
+        starts[e] = free[idx[:N]]
+        goals[e] = free[idx[N:]]
+    return grids, starts, goals
+
+
+@pytest.mark.parametrize("H,W,N,s,K,shared,density", [
+    (12, 12, 10, 7, 60, False, 0.2),
+    (9, 13, 30, 4, 90, True, 0.1),      # crowded, even window, non-square
+    (40, 33, 100, 11, 150, False, 0.15),  # N > 64 (agent loops), s*s > 64
+    (128, 128, 255, 32, 40, True, 0.1),   # the ABI limits: N 255, H*W 16384, s 32
+])
+def test_primal_batch_matches_oracle(mapfx_mod, H, W, N, s, K, shared, density):
+    from oracle.primal_dyn_oracle import PrimalWorld
+    rng = np.random.default_rng(H * 1000 + N)
+    E = 64
+    grids, starts, goals = _random_worlds(rng, E, H, W, N, density, shared)
+    ids = rng.integers(1, N + 1, size=(E, K)).astype(np.int32)
+    # bias toward moves (1..4); some stays
+    acts = rng.choice(5, size=(E, K), p=[0.1, 0.225, 0.225, 0.225, 0.225]).astype(np.int32)
+    b = mapfx_mod.PrimalBatch(starts, goals, grids=grids, observation_size=s)
+    o = {k: _np(v).copy() for k, v in b.act(ids, acts).items()}
+    pos = _np(b.pos)
+    b.check_err()
+    for e in list(range(0, E, 16)) + [E - 1]:
+        w = PrimalWorld(grids[0 if shared else e], starts[e], goals[e], s)
+        for k in range(K):
+            maps, vec, r, done, mask, on_goal, _, valid = w.step(int(ids[e, k]) - 1, int(acts[e, k]))
+            assert np.float64(r).view(np.uint64) == o["reward"][e, k].view(np.uint64), (e, k)
+            assert done == bool(o["done"][e, k]) and mask == int(o["next_mask"][e, k]), (e, k)
+            assert on_goal == bool(o["on_goal"][e, k]) and valid == bool(o["valid"][e, k]), (e, k)
+            assert np.array_equal(maps, o["obs"][e, k]), (e, k)
+            assert np.array_equal(vec.view(np.uint64), o["vec"][e, k].view(np.uint64)), (e, k)
+        assert np.array_equal(np.array(w.pos), pos[e]), e
+
+
+def test_primal_done_when_all_on_goals(mapfx_mod):
+    """Agents already on their goals: staying is status 1 (GOAL_REWARD) and done."""
+    g = np.zeros((4, 4), np.int8)
+    st = np.array([[[0, 0], [3, 3]]], np.int32)
+    b = mapfx_mod.PrimalBatch(st, st, grids=g, observation_size=3)
+    o = b.act([[1, 2, 1]], [[0, 0, 1]])
+    assert _np(o["reward"])[0].tolist() == [0.0, 0.0, -0.3]
+    assert _np(o["done"])[0].tolist() == [1, 1, 0]
+    assert _np(o["valid"])[0].tolist() == [1, 1, 1]
+
+
+def test_primal_bad_call_sets_err(mapfx_mod):
+    g = np.zeros((4, 4), np.int8)
+    b = mapfx_mod.PrimalBatch([[[0, 0]], [[1, 1]]], [[[3, 3]], [[2, 2]]], grids=g[None],
+                              observation_size=3)
+    b.act([[1, 1], [1, 2]], [[1, 2], [0, 0]])  # world 1: agent id 2 does not exist
+    with pytest.raises(AssertionError, match="world 1"):
+        b.check_err()
+    b.act([[1], [1]], [[0], [5]])  # action 5 (diagonal) not available
+    with pytest.raises(AssertionError, match="world 1"):
+        b.check_err()
+
+
+def test_primal_rejects_bad_placement(mapfx_mod):
+    g = np.zeros((4, 4), np.int8)
+    g[1, 1] = -1
+    with pytest.raises(ValueError):
+        mapfx_mod.PrimalBatch([[[1, 1]]], [[[0, 0]]], grids=g)
+    with pytest.raises(ValueError):
+        mapfx_mod.PrimalBatch([[[0, 0], [0, 0]]], [[[2, 2], [3, 3]]], grids=g)

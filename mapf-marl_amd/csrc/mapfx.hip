@@ -99,6 +99,7 @@ struct Geo {
   int wave_ok, EPW;
   int wv_off_map, wv_off_dep, wv_off_bits, wv_off_rew, wv_off_stage, wv_lds;
   int wv_bits_env_bytes, wv_rew_buf, wv_stage_buf, wv_rew_row;  // rew / staging are double-buffered
+  int wv_off_split, wv_split_buf;  // store-wave split: double-buffered per-step output image
 };
 
 struct Args {
@@ -646,6 +647,19 @@ __device__ inline void build_map_rows_c(const Geo& g, uint32_t* map32, uint32_t*
   }
 }
 
+// Workgroups are dealt round-robin to the 8 XCDs (block b runs on XCD b % 8), each
+// with its own L2.  Renumber them so that XCD x owns one contiguous run of env
+// groups: neighbouring groups' small per-step outputs (node / edge / avail / done
+// bytes, rewards) share 128-B lines, which then fill in one L2 instead of leaving
+// two XCDs as partial-line writes.  Identity when the grid is not a multiple of 8.
+#ifndef MAPFX_XCD
+#define MAPFX_XCD 1
+#endif
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  if (!MAPFX_XCD || (nb & 7) != 0) return b;
+  return (b & 7) * (nb >> 3) + (b >> 3);
+}
+
 __device__ inline void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -790,6 +804,206 @@ __device__ __forceinline__ void stage_record(const uint32_t (&R)[4 * WIN], unsig
   *(lds_u16*)(uintptr_t)(ra + (odd ? 0 : REC - 2)) = (uint16_t)(odd ? w[0] : w[NW - 1]);
 }
 
+// One agent's window record registers R ([plane][cols 0-3 | cols 4-7][row]) from its
+// raw post-step map rows: qx[y] = cells 0-3, qx[WIN + y] = cells 4-7, qx[2 WIN + y]
+// = cells 8-11 of window row y, each starting `o` bytes into the first word.
+template <int WIN>
+__device__ __forceinline__ void window_regs(const uint32_t* qx, int o, uint32_t (&R)[4 * WIN]) {
+  uint32_t X0[WIN];
+#pragma unroll
+  for (int y = 0; y < WIN; ++y) {
+    X0[y] = __builtin_amdgcn_alignbyte(qx[WIN + y], qx[y], o);  // cells 0-3
+    swar_window(X0[y], R[y], R[2 * WIN + y]);
+    R[WIN + y] = R[3 * WIN + y] = 0;
+  }
+  if constexpr (WIN == 5) {  // column 4 of rows 0-3 (and of row 4) in one register
+    const uint32_t o4 = (uint32_t)o * 0x0101u;
+    const uint32_t c0 = __builtin_amdgcn_perm(qx[WIN + 1], qx[WIN + 0], 0x0C0C0400u + o4) |
+                        __builtin_amdgcn_perm(qx[WIN + 3], qx[WIN + 2], 0x04000C0Cu + (o4 << 16));
+    const uint32_t c1 = __builtin_amdgcn_alignbyte(0u, qx[WIN + 4], o);
+    swar_window(c0, R[WIN + 0], R[3 * WIN + 0]);
+    swar_window(c1, R[WIN + 1], R[3 * WIN + 1]);
+  } else if constexpr (WIN > 5) {
+#pragma unroll
+    for (int y = 0; y < WIN; ++y)
+      swar_window(__builtin_amdgcn_alignbyte(qx[2 * WIN + y], qx[WIN + y], o), R[WIN + y],
+                  R[3 * WIN + y]);  // cells 4-7
+  }
+}
+
+// ---- store-wave split (runner rollout, N = 16) --------------------------------
+// The wave that steps the envs (the "step wave") keeps only the dependency chain
+// of a step: moves, LDS count atomics, edge collisions (a cross-lane scan) and
+// the dones.  For every agent it hands a 16-byte "info" word (new cell, carried
+// neighbour bytes, flags, edge count, t) and its raw post-step window rows to a
+// second wave of the workgroup (the "store wave") through a double-buffered LDS
+// image.  The store wave derives every output from them -- window record, node
+// collision, avail mask, (row, col), the fp64 reward and its agent-order fold --
+// and writes all of it to HBM (records through an LDS image with lane-contiguous
+// 16-byte stores).  One workgroup barrier per step hands an image over: the step
+// wave fills image s & 1 with step s-1 during step s, while the store wave
+// drains image (s-1) & 1.  The chip then carries two waves per SIMD, and the
+// step wave issues no global store inside its loop.
+#ifndef MAPFX_SPLIT
+#define MAPFX_SPLIT 1  // store-wave split for the N = 16 runner rollout
+#endif
+#ifndef MAPFX_SPLIT_NT
+#define MAPFX_SPLIT_NT 1  // nontemporal (streaming) stores from the store wave
+#endif
+
+template <int WIN, int LL>
+struct SplitLayout {
+  static constexpr int REC = 2 * WIN * WIN;             // window record bytes per agent
+  static constexpr int NXW = (WIN > 5 ? 3 : 2) * WIN;  // raw row words per agent
+  static constexpr int SLOT = (4 + NXW + 3) / 4 * 16;   // info u32x4 + raw rows, per agent
+  static constexpr int BYTES = 64 * SLOT;               // one image (64 agents)
+  static constexpr int STORE_LDS = 2 * (64 * REC + 64 * 8);  // store wave: 2 x (records + reward row)
+  static_assert(LL == 16, "4 envs of 16 agents per wave");
+};
+
+// info.z flag bits
+constexpr uint32_t SF_DONE = 1, SF_LIVE = 2, SF_DNOLD = 4, SF_ENVC = 8, SF_SKIP = 16, SF_OBST = 32,
+                   SF_ALLDONE = 64;
+
+// Workgroup barrier that waits for this wave's LDS traffic only: outstanding
+// global stores stay in flight (a __syncthreads() would drain them every step).
+__device__ __forceinline__ void split_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <typename P, typename V>
+__device__ __forceinline__ void split_store(P p, V v) {
+  if (MAPFX_SPLIT_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// padded LDS cell index -> (row, col); cell < 2^16, pitch < 256
+__device__ __forceinline__ int2 padded_cell_rc(const Geo& g, int cell) {
+  const uint32_t pr = (uint32_t)(((uint64_t)(((uint32_t)cell << 8) & 0xFFFFFFu) *
+                                  (uint64_t)(g.m_pitch24 & 0xFFFFFFu)) >> 32);
+  return make_int2((int)pr - g.P, cell - (int)pr * g.pitch - g.pl);
+}
+
+// Store wave, software-pipelined by one step: after the barrier that hands over
+// step q's image it issues, together, the reads of that image and of its own
+// LDS images of step q-1 (staged window records, per-agent reward row); then it
+// writes step q-1's records and folds step q-1's reward while deriving step q's
+// outputs, so each step costs it one LDS round trip.
+template <int WIN, int LL>
+__device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, unsigned char* sp,
+                                                 int env0, int lane) {
+  typedef __attribute__((address_space(1))) unsigned char gbyte;  // global_store, not flat_
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef int i32x2 __attribute__((ext_vector_type(2)));
+  using SL = SplitLayout<WIN, LL>;
+  constexpr int H2 = WIN / 2, REC = SL::REC, NQ = SL::SLOT / 16;
+  constexpr int RCH = 4 * REC;                  // 16-byte chunks of the wave's 64 records
+  constexpr int NRC = (RCH + 63) / 64;          // chunk rounds per lane
+  constexpr int IMG = SL::STORE_LDS / 2;        // one store-wave image: records + reward row
+  const int T = a.T;
+  const uint32_t E = (uint32_t)g.E, EN = E * (uint32_t)LL;
+  const int slot = lane / LL, ag = lane % LL;
+  const uint32_t env = (uint32_t)(env0 + slot), ag0 = (uint32_t)env0 * LL;
+  unsigned char* own = sp + 2 * g.wv_split_buf;  // 2 images of [64 * REC records | 64 doubles]
+
+  // step p's staged records and reward row (image p & 1) -> HBM; env outputs of p
+  uint32_t p_fl = 0;
+  int p_tcur = 0;
+  auto finish = [&](uint32_t p, const u32x4 (&rv)[NRC], const double (&v)[LL]) {
+    gbyte* rec = (gbyte*)a.obs_window + (p * EN + ag0) * (uint32_t)REC;
+#pragma unroll
+    for (int k = 0; k < NRC; ++k)
+      if (k < NRC - 1 || lane + 64 * k < RCH)
+        split_store((__attribute__((address_space(1))) u32x4*)(rec + 16u * (lane + 64 * k)), rv[k]);
+    if (ag == 0) {  // `sum(rewards)` (:141): naive left fold in agent order
+      double Rs = 0.0;
+#pragma unroll
+      for (int j = 0; j < LL; ++j) Rs = Rs + v[j];
+      const uint32_t ei = p * E + env;
+      split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), Rs);
+      split_store((__attribute__((address_space(1))) int*)((gbyte*)a.traj_t + 4u * ei), p_tcur);
+      split_store((gbyte*)a.term + ei, (unsigned char)((p_fl & SF_ALLDONE) ? 1 : 0));
+      if (a.reward_f32) a.reward_f32[ei] = (float)Rs;
+      if (a.err && (p_fl & SF_SKIP)) atomicCAS(a.err, 0, (int)env + 1);
+    }
+  };
+  auto read_own = [&](uint32_t p, u32x4 (&rv)[NRC], double (&v)[LL]) {
+    const unsigned char* im = own + (p & 1) * IMG;
+    const u32x4* st = (const u32x4*)__builtin_assume_aligned(im, 16);
+#pragma unroll
+    for (int k = 0; k < NRC; ++k) rv[k] = st[(k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0];
+    const double* r = (const double*)(im + 64 * REC) + slot * LL;
+#pragma unroll
+    for (int j = 0; j < LL; ++j) v[j] = r[j];
+  };
+
+  const int rounds = T > 0 ? T + 1 : 0;
+  for (int s = 1; s <= rounds; ++s) {
+    split_barrier();
+    if (s == 1 || (MAPFX_ABLATE & 256)) continue;
+    const uint32_t q = (uint32_t)(s - 2);  // the step image (s - 1) & 1 carries
+    const u32x4* sl = (const u32x4*)__builtin_assume_aligned(
+        sp + ((s - 1) & 1) * g.wv_split_buf + lane * SL::SLOT, 16);
+    uint32_t w[4 * NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const u32x4 v = sl[i];
+      w[4 * i] = v.x;
+      w[4 * i + 1] = v.y;
+      w[4 * i + 2] = v.z;
+      w[4 * i + 3] = v.w;
+    }
+    u32x4 rv[NRC];
+    double pv[LL];
+    if (q > 0) read_own(q - 1, rv, pv);
+    const int nc = (int)w[0];
+    const uint32_t nb = w[1], fl = w[2];
+    const uint32_t* qx = w + 4;
+    const int o = (nc - H2) & 3;
+    uint32_t R[4 * WIN];
+    window_regs<WIN>(qx, o, R);
+    // node collision (:344-362): post-step count = c - 1 + obstacle >= 2 (centre cell)
+    const uint32_t ctr = (__builtin_amdgcn_alignbyte(qx[WIN + H2], qx[H2], o) >> (8 * H2)) & 0xFFu;
+    uint32_t node = ctr + ((fl / SF_OBST) & 1u) >= 3u ? 1u : 0u;
+    if (fl & SF_SKIP) node = 0;
+    // avail (:203-224): a neighbour is available iff its c != 0; stay always
+    const uint32_t nzn = ((nb + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
+    const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
+    const uint32_t edge = fl >> 8;
+    // reward (:94-130, exact fp64 op order)
+    double rr = 0.0;
+    if (fl & SF_LIVE) {
+      if (!(fl & SF_DNOLD)) {
+        if (fl & SF_ENVC) rr = rr + g.collide_rew;
+        rr = rr + g.step_rew;
+      }
+      rr = rr + g.collide_rew * (double)node;
+      rr = rr + g.collide_rew * (double)edge;
+    }
+    if (q > 0) finish(q - 1, rv, pv);
+    unsigned char* im = own + (q & 1) * IMG;
+    stage_record<WIN>(R, im + lane * REC);
+    ((double*)(im + 64 * REC))[lane] = rr;
+    const uint32_t ai = q * EN + ag0 + lane;
+    const int2 rc = padded_cell_rc(g, nc);
+    split_store((__attribute__((address_space(1))) i32x2*)((gbyte*)a.traj_pos + 8u * ai),
+                i32x2{rc.x, rc.y});
+    split_store((gbyte*)a.node + ai, (unsigned char)node);
+    split_store((gbyte*)a.edge + ai, (unsigned char)edge);
+    split_store((gbyte*)a.avail + ai, (unsigned char)availm);
+    split_store((gbyte*)a.traj_done + ai, (unsigned char)(fl & SF_DONE));
+    p_fl = fl;
+    p_tcur = (int)w[3];
+  }
+  if (T > 0 && !(MAPFX_ABLATE & 256)) {  // the last step's records and reward
+    wave_fence();
+    u32x4 rv[NRC];
+    double pv[LL];
+    read_own((uint32_t)(T - 1), rv, pv);
+    finish((uint32_t)(T - 1), rv, pv);
+  }
+}
+
 // FULLW: every lane owns an agent (N == L and E % EPW == 0) -> no lane masks.
 // RUNNER (rollout only): the standard runner outputs are all present (reward,
 // term, node, edge, avail, traj_pos/done/t, window obs) -> no per-output tests.
@@ -806,9 +1020,17 @@ __device__ __forceinline__ void stage_record(const uint32_t (&R)[4 * WIN], unsig
 //   D  step s's neighbour bytes, dones, t and all-done ballot  (dependency chain)
 // so only A and D (a few dozen instructions) sit on the serial chain between
 // steps.  The last step's heavy part and tails run after the loop.
-template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL>
-__global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
+template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false>
+__global__ void __launch_bounds__(SPLIT ? 128 : 64) mapf_wave_kernel(Geo g, Args a) {
   extern __shared__ __align__(16) unsigned char lds[];
+  static_assert(!SPLIT || (ROLL && FULLW && RUNNER && LL == 16 && WIN > 0), "split: runner rollout, N = 16");
+  if constexpr (SPLIT) {
+    if (threadIdx.x >= 64) {  // the store wave
+      split_store_wave<WIN, LL>(g, a, lds + g.wv_off_split, xcd_block(blockIdx.x, gridDim.x) * (64 / LL),
+                                (int)threadIdx.x - 64);
+      return;
+    }
+  }
   constexpr int WW = WIN * WIN;
   constexpr int H2 = WIN / 2;
   constexpr int REC = 2 * WW;  // record bytes per agent
@@ -821,12 +1043,12 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   const int L = LL > 0 ? LL : g.L;
   const int lshift = LL > 0 ? (LL == 64 ? 6 : LL == 32 ? 5 : LL == 16 ? 4 : LL == 8 ? 3 : LL == 4 ? 2 : LL == 2 ? 1 : 0)
                             : g.lshift;
-  const int lane64 = threadIdx.x;
+  const int lane64 = threadIdx.x & 63;
   const int slot = lane64 >> lshift;  // env slot within the wave
   const int ag = lane64 & (L - 1);    // agent index
   const int base = slot << lshift;    // first lane of this env
   const int EPW = 64 >> lshift;
-  const int env0 = blockIdx.x * EPW;
+  const int env0 = xcd_block(blockIdx.x, gridDim.x) * EPW;
   const int env = env0 + slot;
   const int N = FIXN ? LL : g.N;
   const bool env_ok = FULLW || env < g.E;
@@ -962,35 +1184,58 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   bool p_skip = false, p_alldone = false;
   int p_tcur = 0;
 
+  // edge collisions (:364-383) of step q: i moved into a cell X that had pre-step
+  // occupants; j counts iff j moved from X back into i's old cell, i.e. in the
+  // opposite direction (act ^ 1)
+  auto edge_of = [&]() {
+    int edge = 0;
+    const bool suspect = q_moved && q_pre > 0;
+    if (__ballot(suspect)) {
+      if (suspect && q_pre == 1) edge = (q_dj & 0x7Fu) == (uint32_t)(q_act ^ 1) ? 1 : 0;
+      if (__ballot(suspect && q_pre > 1)) {  // stacked pre-occupants: scan the env
+        for (int j = 0; j < N; ++j) {
+          const int oj2 = __shfl(q_oc, base + j);
+          const int nj2 = __shfl(q_nc, base + j);
+          if (suspect && q_pre > 1) edge += (oj2 == q_nc) & (nj2 == q_oc);
+        }
+      }
+    }
+    return edge;
+  };
+
   // HEAVY part of step q (slot qs): window, node, edge, reward, per-agent stores.
   auto heavy = [&](int qs) {
+    if constexpr (SPLIT) {  // step q's info word and raw window rows -> image (qs + 1) & 1
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      using SL = SplitLayout<WIN, LL>;
+      const int edge = edge_of();
+      u32x4* sl = (u32x4*)__builtin_assume_aligned(
+          lds + g.wv_off_split + ((qs + 1) & 1) * g.wv_split_buf + lane64 * SL::SLOT, 16);
+      const uint32_t fl = (q_dn ? SF_DONE : 0u) | (q_live ? SF_LIVE : 0u) | (q_dnold ? SF_DNOLD : 0u) |
+                          (q_envc ? SF_ENVC : 0u) | (q_skip ? SF_SKIP : 0u) | ((q_dj >> 7) ? SF_OBST : 0u) |
+                          (q_alldone ? SF_ALLDONE : 0u) | ((uint32_t)(edge > 255 ? 255 : edge) << 8);
+      uint32_t w[SL::SLOT / 4];
+      w[0] = (uint32_t)q_nc;
+      w[1] = q_nb;
+      w[2] = fl;
+      w[3] = (uint32_t)q_tcur;
+#pragma unroll
+      for (int i = 0; i < SL::NXW; ++i) w[4 + i] = qx[i];
+#pragma unroll
+      for (int i = 4 + SL::NXW; i < SL::SLOT / 4; ++i) w[i] = 0;
+#pragma unroll
+      for (int i = 0; i < SL::SLOT / 16; ++i) sl[i] = u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+      return;
+    }
     const uint32_t so = ROLL ? (uint32_t)qs * EN : 0u;
     const int buf = ROLL ? (qs & 1) : 0;
     uint32_t node = 0;
     uint32_t R[WIN > 0 ? 4 * WIN : 1];  // [plane][cols 0-3 | cols 4-7][row]
     if constexpr (WIN > 0) {
       const int o = (q_nc - H2) & 3;  // same byte offset in every row (pitch % 4 == 0)
-      uint32_t X0[WIN];
-#pragma unroll
-      for (int y = 0; y < WIN; ++y) {
-        X0[y] = __builtin_amdgcn_alignbyte(qx[WIN + y], qx[y], o);  // cells 0-3
-        swar_window(X0[y], R[y], R[2 * WIN + y]);
-        R[WIN + y] = R[3 * WIN + y] = 0;
-      }
-      if constexpr (WIN == 5) {  // column 4 of rows 0-3 (and of row 4) in one register
-        const uint32_t o4 = (uint32_t)o * 0x0101u;
-        const uint32_t c0 = __builtin_amdgcn_perm(qx[WIN + 1], qx[WIN + 0], 0x0C0C0400u + o4) |
-                            __builtin_amdgcn_perm(qx[WIN + 3], qx[WIN + 2], 0x04000C0Cu + (o4 << 16));
-        const uint32_t c1 = __builtin_amdgcn_alignbyte(0u, qx[WIN + 4], o);
-        swar_window(c0, R[WIN + 0], R[3 * WIN + 0]);
-        swar_window(c1, R[WIN + 1], R[3 * WIN + 1]);
-      } else if constexpr (WIN > 5) {
-#pragma unroll
-        for (int y = 0; y < WIN; ++y)
-          swar_window(__builtin_amdgcn_alignbyte(qx[2 * WIN + y], qx[WIN + y], o), R[WIN + y],
-                      R[3 * WIN + y]);  // cells 4-7
-      }
-      const uint32_t ctr = (X0[H2] >> (8 * H2)) & 0xFFu;  // H2 <= 3: centre is in cells 0-3
+      window_regs<WIN>(qx, o, R);
+      // centre cell (H2 <= 3: it lies in cells 0-3 of the middle row)
+      const uint32_t ctr = (__builtin_amdgcn_alignbyte(qx[WIN + H2], qx[H2], o) >> (8 * H2)) & 0xFFu;
       node = ctr + (q_dj >> 7) >= 3u ? 1u : 0u;            // count = c - 1 + obstacle >= 2
     } else {
       node = (qx[0] & 0xFFu) + (q_dj >> 7) >= 3u ? 1u : 0u;
@@ -1036,21 +1281,7 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
         if (a.avail) a.avail[ai] = (uint8_t)availm;
       }
     }
-    // edge collisions (:364-383): i moved into a cell X that had pre-step
-    // occupants; j counts iff j moved from X back into i's old cell, i.e. in the
-    // opposite direction (act ^ 1)
-    int edge = 0;
-    const bool suspect = q_moved && q_pre > 0;
-    if (__ballot(suspect)) {
-      if (suspect && q_pre == 1) edge = (q_dj & 0x7Fu) == (uint32_t)(q_act ^ 1) ? 1 : 0;
-      if (__ballot(suspect && q_pre > 1)) {  // stacked pre-occupants: scan the env
-        for (int j = 0; j < N; ++j) {
-          const int oj2 = __shfl(q_oc, base + j);
-          const int nj2 = __shfl(q_nc, base + j);
-          if (suspect && q_pre > 1) edge += (oj2 == q_nc) & (nj2 == q_oc);
-        }
-      }
-    }
+    const int edge = edge_of();
     // reward (:94-130, exact fp64 op order)
     double rr = 0.0;
     if (q_live) {
@@ -1165,10 +1396,11 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
       xr = map[nc + 1];
     }
     const uint32_t dj = (MAPFX_ABLATE & 64) ? 0xFFu : dep[nc];  // pre-step occupant's move
-    const double Rp = (ROLL && do_step) ? fold(s & 1) : 0.0;     // step s-2's row
+    const double Rp = (!SPLIT && ROLL && do_step) ? fold(s & 1) : 0.0;  // step s-2's row
+    STAMP(1);
     // ---------------- C: heavy part of step s-1, env outputs of step s-2 -----------
     if (s > 0) heavy(s - 1);
-    if (ROLL && s > 1) tail(s & 1, p_se, p_skip, p_alldone, p_tcur, Rp);
+    if (!SPLIT && ROLL && s > 1) tail(s & 1, p_se, p_skip, p_alldone, p_tcur, Rp);
     STAMP(3);
     // ---------------- D: step s's neighbours, dones, t (:112-117) ----------------
     uint32_t nbn;
@@ -1252,7 +1484,9 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
         f_cur = (uint32_t)dep[cur] >> 7;
       }
     }
-    wave_fence();
+    STAMP(4);
+    if constexpr (SPLIT) split_barrier();  // image s & 1 -> store wave
+    else wave_fence();
     STAMP(6);
   }
 #ifdef MAPFX_CLOCKS
@@ -1269,7 +1503,10 @@ __global__ void __launch_bounds__(64) mapf_wave_kernel(Geo g, Args a) {
   }
 #endif
   // ---- drain the pipeline: heavy part of the last step, the last two tails ----
-  if (T > 0) {
+  if (SPLIT && T > 0) {
+    heavy(T - 1);
+    split_barrier();  // image T & 1: the last step
+  } else if (T > 0) {
     const double Rp = (ROLL && T > 1) ? fold(T & 1) : 0.0;  // step T-2's row
     heavy(T - 1);
     if (ROLL && T > 1) tail(T & 1, p_se, p_skip, p_alldone, p_tcur, Rp);
@@ -1372,10 +1609,14 @@ int check_hip(hipError_t e, const char* what) {
   return MAPFX_OK;
 }
 
+
 template <int WIN>
-KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L) {
+KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split) {
   if (roll) {
     if (runner) {
+      if constexpr (WIN > 0) {
+        if (split && fullw && L == 16) return mapf_wave_kernel<WIN, true, true, true, 16, true>;
+      }
       if (!fullw) return mapf_wave_kernel<WIN, true, false, true, 0>;
       if (L == 16) return mapf_wave_kernel<WIN, true, true, true, 16>;
       if (L == 64) return mapf_wave_kernel<WIN, true, true, true, 64>;
@@ -1387,12 +1628,12 @@ KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L) {
   return fullw ? mapf_wave_kernel<WIN, false, true, false, 0> : mapf_wave_kernel<WIN, false, false, false, 0>;
 }
 
-KernelFn pick_wave_kernel(int win, bool roll, bool fullw, bool runner, int L) {
+KernelFn pick_wave_kernel(int win, bool roll, bool fullw, bool runner, int L, bool split) {
   switch (win) {
-    case 0: return pick_wave_win<0>(roll, fullw, runner, L);
-    case 3: return pick_wave_win<3>(roll, fullw, runner, L);
-    case 5: return pick_wave_win<5>(roll, fullw, runner, L);
-    case 7: return pick_wave_win<7>(roll, fullw, runner, L);
+    case 0: return pick_wave_win<0>(roll, fullw, runner, L, split);
+    case 3: return pick_wave_win<3>(roll, fullw, runner, L, split);
+    case 5: return pick_wave_win<5>(roll, fullw, runner, L, split);
+    case 7: return pick_wave_win<7>(roll, fullw, runner, L, split);
   }
   return nullptr;
 }
@@ -1408,10 +1649,17 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream) {
     const bool fullw = g.N == g.L && g.E % g.EPW == 0;
     const bool runner = roll && a.reward && a.term && a.node && a.edge && a.avail &&
                         a.traj_pos && a.traj_done && a.traj_t && a.obs_window && !a.obs_full;
-    KernelFn fn = pick_wave_kernel(a.obs_window ? g.window : 0, roll, fullw, runner, g.L);
+    const uintptr_t al16 = (uintptr_t)a.obs_window | (uintptr_t)a.traj_pos | (uintptr_t)a.node |
+                           (uintptr_t)a.edge | (uintptr_t)a.avail | (uintptr_t)a.traj_done |
+                           (uintptr_t)a.reward | (uintptr_t)a.traj_t;
+    const int split_lds = g.wv_lds + 2 * g.wv_split_buf + 2 * (64 * g.wlen + 64 * 8);  // + store-wave images
+    const bool split = MAPFX_SPLIT && runner && fullw && g.L == 16 && g.wv_split_buf > 0 &&
+                       split_lds <= 64 * 1024 && (al16 & 15) == 0;
+    KernelFn fn = pick_wave_kernel(a.obs_window ? g.window : 0, roll, fullw, runner, g.L, split);
     if (fn) {
       const int blocks = (g.E + g.EPW - 1) / g.EPW;
-      hipLaunchKernelGGL(fn, dim3(blocks), dim3(64), g.wv_lds, stream, g, a);
+      hipLaunchKernelGGL(fn, dim3(blocks), dim3(split ? 128 : 64),
+                         split ? split_lds : g.wv_lds, stream, g, a);
       return check_hip(hipGetLastError(), "mapf_wave_kernel launch");
     }
   }
@@ -1652,6 +1900,11 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     g.wv_off_stage = o;
     o += 2 * g.wv_stage_buf;
     g.wv_lds = o;
+    // store-wave split images (placed after the wave layout; only that kernel allocates them)
+    g.wv_off_split = o;
+    g.wv_split_buf = L != 16 ? 0 : c.window == 3 ? SplitLayout<3, 16>::BYTES
+                                 : c.window == 5 ? SplitLayout<5, 16>::BYTES
+                                 : c.window == 7 ? SplitLayout<7, 16>::BYTES : 0;
     g.wave_ok = (o <= 64 * 1024 && pitch < 256 && g.rows * pitch < 65536) ? 1 : 0;
   }
 

@@ -213,6 +213,43 @@ def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T, obs, win):
         assert np.array_equal(_np(bb.steps), _np(b3.steps))
 
 
+@pytest.mark.parametrize("E,T,win,autoreset", [
+    (4096, 64, 5, False),   # the bench shape
+    (256, 1, 5, False), (256, 2, 5, False), (256, 3, 3, False), (252, 17, 7, False),
+    (64, 40, 5, True)])
+def test_runner_rollout_every_step(mapfx_mod, E, T, win, autoreset):
+    """N = 16 runner rollouts (every PyMARL output, no full map) take the store-wave
+    kernel: each step's outputs must equal one step launch's, step by step."""
+    from mapfx.maps import synthetic_instances
+    S, N = 32 if not autoreset else 8, 16
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=12)
+    kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=2000 if not autoreset else 9,
+              obs=("window",), window=win)
+    b1 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
+    b2 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
+    b1.reset()
+    b2.reset()
+    acts = b2.gen_actions(T, 21, t0=0)
+    traj = b1.rollout(T, actions=acts, autoreset=autoreset)
+    keys = ("reward", "reward_f32", "term", "node", "edge", "avail", "obs_window")
+    for k in range(T):
+        out = b2.step(acts[k])
+        for key in keys:
+            x, y = _np(out[key]), _np(traj[key][k])
+            if x.dtype == np.float64:
+                assert np.array_equal(_u64(x), _u64(y)), (key, k)
+            else:
+                assert np.array_equal(x, y), (key, k)
+        assert np.array_equal(_np(traj["traj_pos"][k]), _np(b2.pos)), k
+        assert np.array_equal(_np(traj["traj_done"][k]), _np(b2.done)), k
+        assert np.array_equal(_np(traj["traj_t"][k]), _np(b2.t)), k
+        if autoreset and out["term"].any():
+            b2.reset(env_mask=out["term"].clone())
+    assert np.array_equal(_np(b1.pos), _np(b2.pos))
+    assert np.array_equal(_np(b1.done), _np(b2.done))
+    assert np.array_equal(_np(b1.t), _np(b2.t))
+
+
 def test_rollout_matches_oracle_long_horizon(mapfx_mod):
     """C2 shape (32x32, 16 agents, 4096 envs), 64 fused steps vs the C oracle."""
     from mapfx.maps import synthetic_instances

@@ -15,6 +15,7 @@ def main():
     from mapfx.maps import synthetic_instances
     variant = sys.argv[1] if len(sys.argv) > 1 else "all"
     S, N, E, p, _ = bench.CONFIGS["c2"]
+    E = int(os.environ.get("MAPFX_PROBE_E", E))
     inst = synthetic_instances(E, S, S, N, p_obstacle=p, seed=1)
     b = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
                             episode_limit=2 ** 31 - 1, obs=("window",), window=5,

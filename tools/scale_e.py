@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--envs", default="256,1024,2048,4096,8192,16384,32768")
     ap.add_argument("--n", type=int, default=16)
     ap.add_argument("--Ts", default="", help="comma list of T at E=4096 instead of the E sweep")
+    ap.add_argument("--rng", action="store_true", help="device-generated actions (no action loads)")
     a = ap.parse_args()
     import mapfx
     from mapfx.maps import synthetic_instances
@@ -46,7 +47,10 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for i in range(launches):
-                b.rollout(T, actions=acts[i * T:(i + 1) * T], traj=traj, outputs=outs)
+                if a.rng:
+                    b.rollout(T, seed=2, t0=i * T, traj=traj, outputs=outs)
+                else:
+                    b.rollout(T, actions=acts[i * T:(i + 1) * T], traj=traj, outputs=outs)
             e1.record()
             torch.cuda.synchronize()
             res.append(e0.elapsed_time(e1) / (launches * T) * 1e3)

@@ -1,11 +1,15 @@
 #!/usr/bin/env python3
-"""Per-segment cycle shares of one rollout step (diagnostic build libmapfx_stamps.so)."""
+"""Per-segment cycle counts of one rollout step, block 0 / lane 0 (diagnostic build
+libmapfx_stamps.so: tools/build_variant.sh stamps "" -DMAPFX_STAMPS).
+
+  MAPFX_PROBE_E=4096 python tools/stamps.py
+"""
 import ctypes
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["MAPFX_LIB"] = os.path.join(REPO, "mapf-marl_amd", "mapfx", "libmapfx_stamps.so")
+os.environ.setdefault("MAPFX_LIB", os.path.join(REPO, "mapf-marl_amd", "mapfx", "libmapfx_stamps.so"))
 sys.path[:0] = [REPO, os.path.join(REPO, "mapf-marl_amd")]
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -16,6 +20,7 @@ def main():
     import mapfx
     from mapfx.maps import synthetic_instances
     S, N, E, p, _ = bench.CONFIGS["c2"]
+    E = int(os.environ.get("MAPFX_PROBE_E", E))
     inst = synthetic_instances(E, S, S, N, p_obstacle=p, seed=1)
     b = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
                             episode_limit=2 ** 31 - 1, obs=("window",), window=5, track_steps=False)
@@ -23,7 +28,6 @@ def main():
     T = 64
     acts = b.gen_actions(T * 3, seed=2)
     traj = b._alloc_out(T)
-    traj.pop("reward_f32")
     outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done", "traj_t")
     for i in range(3):
         b.rollout(T, actions=acts[i * T:(i + 1) * T], traj=traj, outputs=outs)
@@ -31,19 +35,17 @@ def main():
     buf = (ctypes.c_ulonglong * (256 * 8))()
     mapfx.lib.mapfx_debug_stamps.restype = ctypes.c_int
     assert mapfx.lib.mapfx_debug_stamps(buf) == 0
-    st8 = np.array(buf, dtype=np.int64).reshape(256, 8)[:T]
-    st = st8[:, [0, 7, 1, 2, 3, 4, 5, 6]]
-    names = ["cand read", "tail(prev)", "move+atomics", "edge", "rows/window", "reward+stage",
-             "stores+fence"]
-    d = np.diff(st, axis=1)
-    nxt = st[1:, 0] - st[:-1, 6]
-    print("per-step cycles (median over steps 1..T-1)")
-    for k in range(d.shape[1]):
-        print("  %-16s median %6.0f  mean %6.0f" % (names[k], np.median(d[1:, k]), d[1:, k].mean()))
-    nxt = st[1:, 0] - st[:-1, -1]
-    print("  %-16s median %6.0f  mean %6.0f" % ("fence+loop+acts", np.median(nxt), nxt.mean()))
-    tot = st[1:, 0] - st[:-1, 0]
-    print("  step total       median %6.0f  mean %6.0f  (steps%%16==0: %s)" % (np.median(tot), tot.mean(), tot[15::16]))
+    st = np.array(buf, dtype=np.int64).reshape(256, 8)[:T]
+    order = [0, 2, 1, 3, 4, 6]
+    names = ["A move+atomics", "B rows+fold", "C heavy+tail", "D nbrs+dones", "end barrier/fence"]
+    print("E=%d  s_memtime cycles per step segment (median / mean over steps 1..T-2)" % E)
+    for k in range(len(order) - 1):
+        d = st[1:-1, order[k + 1]] - st[1:-1, order[k]]
+        print("  %-18s %7.0f %7.0f" % (names[k], np.median(d), d.mean()))
+    nxt = st[2:, 0] - st[1:-1, 6]
+    print("  %-18s %7.0f %7.0f" % ("loop+actions", np.median(nxt), nxt.mean()))
+    tot = st[2:, 0] - st[1:-1, 0]
+    print("  %-18s %7.0f %7.0f" % ("step total", np.median(tot), tot.mean()))
 
 
 if __name__ == "__main__":

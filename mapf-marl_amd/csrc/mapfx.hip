@@ -850,6 +850,10 @@ __device__ __forceinline__ void window_regs(const uint32_t* qx, int o, uint32_t 
 #ifndef MAPFX_SPLIT_NT
 #define MAPFX_SPLIT_NT 1  // nontemporal (streaming) stores from the store wave
 #endif
+#ifndef MAPFX_SPLIT_DIRECT
+#define MAPFX_SPLIT_DIRECT 0  // 1: store wave writes window records per lane (no LDS image)
+#endif
+
 
 template <int WIN, int LL>
 struct SplitLayout {
@@ -900,6 +904,7 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
   constexpr int RCH = 4 * REC;                  // 16-byte chunks of the wave's 64 records
   constexpr int NRC = (RCH + 63) / 64;          // chunk rounds per lane
   constexpr int IMG = SL::STORE_LDS / 2;        // one store-wave image: records + reward row
+  constexpr bool DIRECT = MAPFX_SPLIT_DIRECT;   // records straight from registers (no image)
   const int T = a.T;
   const uint32_t E = (uint32_t)g.E, EN = E * (uint32_t)LL;
   const int slot = lane / LL, ag = lane % LL;
@@ -909,16 +914,20 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
   // step p's staged records and reward row (image p & 1) -> HBM; env outputs of p
   uint32_t p_fl = 0;
   int p_tcur = 0;
-  auto finish = [&](uint32_t p, const u32x4 (&rv)[NRC], const double (&v)[LL]) {
+  auto finish = [&](uint32_t p, const u32x4 (&rv)[NRC], const double (&v)[LL], bool ok) {
     gbyte* rec = (gbyte*)a.obs_window + (p * EN + ag0) * (uint32_t)REC;
+    if constexpr (!DIRECT) {
 #pragma unroll
-    for (int k = 0; k < NRC; ++k)
-      if (k < NRC - 1 || lane + 64 * k < RCH)
-        split_store((__attribute__((address_space(1))) u32x4*)(rec + 16u * (lane + 64 * k)), rv[k]);
-    if (ag == 0) {  // `sum(rewards)` (:141): naive left fold in agent order
-      double Rs = 0.0;
+      for (int k = 0; k < NRC; ++k)
+        if (ok && (k < NRC - 1 || lane + 64 * k < RCH))
+          split_store((__attribute__((address_space(1))) u32x4*)(rec + 16u * (lane + 64 * k)), rv[k]);
+    }
+    // `sum(rewards)` (:141): naive left fold in agent order -- in every lane, so the
+    // dependent adds share a basic block with (and interleave into) the next step's work
+    double Rs = 0.0;
 #pragma unroll
-      for (int j = 0; j < LL; ++j) Rs = Rs + v[j];
+    for (int j = 0; j < LL; ++j) Rs = Rs + v[j];
+    if (ok && ag == 0) {
       const uint32_t ei = p * E + env;
       split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), Rs);
       split_store((__attribute__((address_space(1))) int*)((gbyte*)a.traj_t + 4u * ei), p_tcur);
@@ -930,8 +939,10 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
   auto read_own = [&](uint32_t p, u32x4 (&rv)[NRC], double (&v)[LL]) {
     const unsigned char* im = own + (p & 1) * IMG;
     const u32x4* st = (const u32x4*)__builtin_assume_aligned(im, 16);
+    if constexpr (!DIRECT) {
 #pragma unroll
-    for (int k = 0; k < NRC; ++k) rv[k] = st[(k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0];
+      for (int k = 0; k < NRC; ++k) rv[k] = st[(k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0];
+    }
     const double* r = (const double*)(im + 64 * REC) + slot * LL;
 #pragma unroll
     for (int j = 0; j < LL; ++j) v[j] = r[j];
@@ -955,7 +966,7 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
     }
     u32x4 rv[NRC];
     double pv[LL];
-    if (q > 0) read_own(q - 1, rv, pv);
+    read_own(q - 1, rv, pv);  // q = 0: stale image, nothing of it is stored
     const int nc = (int)w[0];
     const uint32_t nb = w[1], fl = w[2];
     const uint32_t* qx = w + 4;
@@ -980,11 +991,12 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
       rr = rr + g.collide_rew * (double)node;
       rr = rr + g.collide_rew * (double)edge;
     }
-    if (q > 0) finish(q - 1, rv, pv);
+    finish(q - 1, rv, pv, q > 0);
     unsigned char* im = own + (q & 1) * IMG;
-    stage_record<WIN>(R, im + lane * REC);
-    ((double*)(im + 64 * REC))[lane] = rr;
     const uint32_t ai = q * EN + ag0 + lane;
+    if constexpr (DIRECT) write_record<WIN>(R, a.obs_window, ai * (uint32_t)REC);
+    else stage_record<WIN>(R, im + lane * REC);
+    ((double*)(im + 64 * REC))[lane] = rr;
     const int2 rc = padded_cell_rc(g, nc);
     split_store((__attribute__((address_space(1))) i32x2*)((gbyte*)a.traj_pos + 8u * ai),
                 i32x2{rc.x, rc.y});
@@ -1000,7 +1012,7 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
     u32x4 rv[NRC];
     double pv[LL];
     read_own((uint32_t)(T - 1), rv, pv);
-    finish((uint32_t)(T - 1), rv, pv);
+    finish((uint32_t)(T - 1), rv, pv, true);
   }
 }
 
@@ -1025,9 +1037,9 @@ __global__ void __launch_bounds__(SPLIT ? 128 : 64) mapf_wave_kernel(Geo g, Args
   extern __shared__ __align__(16) unsigned char lds[];
   static_assert(!SPLIT || (ROLL && FULLW && RUNNER && LL == 16 && WIN > 0), "split: runner rollout, N = 16");
   if constexpr (SPLIT) {
-    if (threadIdx.x >= 64) {  // the store wave
-      split_store_wave<WIN, LL>(g, a, lds + g.wv_off_split, xcd_block(blockIdx.x, gridDim.x) * (64 / LL),
-                                (int)threadIdx.x - 64);
+    if (threadIdx.x >= 64) {  // the output side of the split
+      const int e0 = xcd_block(blockIdx.x, gridDim.x) * (64 / LL);
+      split_store_wave<WIN, LL>(g, a, lds + g.wv_off_split, e0, threadIdx.x & 63);
       return;
     }
   }

@@ -853,6 +853,26 @@ __device__ __forceinline__ void window_regs(const uint32_t* qx, int o, uint32_t 
 #ifndef MAPFX_SPLIT_DIRECT
 #define MAPFX_SPLIT_DIRECT 0  // 1: store wave writes window records per lane (no LDS image)
 #endif
+#ifndef MAPFX_SPLIT_DPPFOLD
+#define MAPFX_SPLIT_DPPFOLD 1  // reward fold as an in-row DPP scan (no LDS reward row)
+#endif
+
+// `sum(rewards)` (mapf_gridworld.py:141) over a 16-lane DPP row: a naive left fold
+// ((0 + r_0) + r_1) + ... in agent order.  Iteration k makes lane k's running sum
+// final (each lane adds its own reward to its left neighbour's running sum), so
+// after 15 shifts lane j holds the fold of agents 0..j; lane 0's left input is
+// the bound-control zero, i.e. the fold's initial 0.
+__device__ __forceinline__ double row_fold16(double r) {
+  double R = 0.0 + r;
+#pragma unroll
+  for (int k = 1; k < 16; ++k) {
+    const uint64_t b = (uint64_t)__double_as_longlong(R);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x111, 0xF, 0xF, true);  // row_shr:1
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x111, 0xF, 0xF, true);
+    R = __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo)) + r;
+  }
+  return R;
+}
 
 
 template <int WIN, int LL>
@@ -905,6 +925,7 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
   constexpr int NRC = (RCH + 63) / 64;          // chunk rounds per lane
   constexpr int IMG = SL::STORE_LDS / 2;        // one store-wave image: records + reward row
   constexpr bool DIRECT = MAPFX_SPLIT_DIRECT;   // records straight from registers (no image)
+  constexpr bool DPPFOLD = MAPFX_SPLIT_DPPFOLD;  // fold as an in-row DPP scan, same step
   const int T = a.T;
   const uint32_t E = (uint32_t)g.E, EN = E * (uint32_t)LL;
   const int slot = lane / LL, ag = lane % LL;
@@ -927,7 +948,7 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
     double Rs = 0.0;
 #pragma unroll
     for (int j = 0; j < LL; ++j) Rs = Rs + v[j];
-    if (ok && ag == 0) {
+    if (!DPPFOLD && ok && ag == 0) {
       const uint32_t ei = p * E + env;
       split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), Rs);
       split_store((__attribute__((address_space(1))) int*)((gbyte*)a.traj_t + 4u * ei), p_tcur);
@@ -945,7 +966,7 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
     }
     const double* r = (const double*)(im + 64 * REC) + slot * LL;
 #pragma unroll
-    for (int j = 0; j < LL; ++j) v[j] = r[j];
+    for (int j = 0; j < LL; ++j) v[j] = DPPFOLD ? 0.0 : r[j];
   };
 
   const int rounds = T > 0 ? T + 1 : 0;
@@ -992,6 +1013,17 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
       rr = rr + g.collide_rew * (double)edge;
     }
     finish(q - 1, rv, pv, q > 0);
+    if constexpr (DPPFOLD) {  // `sum(rewards)` (:141); lane LL-1 of the env holds the total
+      const double Rs = row_fold16(rr);
+      if (ag == LL - 1) {
+        const uint32_t ei = q * E + env;
+        split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), Rs);
+        split_store((__attribute__((address_space(1))) int*)((gbyte*)a.traj_t + 4u * ei), (int)w[3]);
+        split_store((gbyte*)a.term + ei, (unsigned char)((fl & SF_ALLDONE) ? 1 : 0));
+        if (a.reward_f32) a.reward_f32[ei] = (float)Rs;
+        if (a.err && (fl & SF_SKIP)) atomicCAS(a.err, 0, (int)env + 1);
+      }
+    }
     unsigned char* im = own + (q & 1) * IMG;
     const uint32_t ai = q * EN + ag0 + lane;
     if constexpr (DIRECT) write_record<WIN>(R, a.obs_window, ai * (uint32_t)REC);

@@ -307,14 +307,16 @@ def run_partial(args, dist, rank, world, local):
     import mapfx
     from mapfx.maps import synthetic_instances
     S, N, E = 8, 15, args.partial_envs
-    K, WU = args.steps, args.warmup
+    limit = PARTIAL_YAML["episode_limit"]
+    # whole episodes: round --steps / --warmup up to multiples of the episode limit
+    K = -(-args.steps // limit) * limit
+    WU = -(-args.warmup // limit) * limit
     offset = rank * E
     inst = synthetic_instances(E, S, S, N, p_obstacle=0.0, seed=1, env_offset=offset)
     grids = np.zeros((1, S, S), dtype=np.int8)
     b = mapfx.MarlPartialBatch(inst["init_pos"], inst["goals"], grids=grids,
                                device="cuda:%d" % local, env_offset=offset, **PARTIAL_YAML)
     b.reset()
-    limit = PARTIAL_YAML["episode_limit"]
     ga = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
                              obs=(), device="cuda:%d" % local, env_offset=offset,
                              track_steps=False)
@@ -325,8 +327,6 @@ def run_partial(args, dist, rank, world, local):
     # One episode (reset + `limit` steps, one kernel launch each) captured once as a
     # HIP graph and replayed: the per-step launches run back to back without the
     # Python / ctypes launch overhead of the drop-in path between them.
-    if K % limit or WU % limit:
-        raise SystemExit("--steps and --warmup must be multiples of the episode limit (%d)" % limit)
     graph = torch.cuda.CUDAGraph()
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())

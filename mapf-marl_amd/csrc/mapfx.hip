@@ -336,15 +336,40 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     __syncthreads();  // B2: post-step map complete
     // ================= P2: collisions, rewards, avail, observations =================
     const long long slotE = ROLL ? (long long)s * Elong : 0;  // trajectory slot offset (envs)
+    // edge collisions (:364-383): i moved into a cell that had pre-step occupants;
+    // count the agents j that moved from that cell into i's old cell.  With whole
+    // waves per env (L >= 64) the wave scans the env's agents together for each
+    // such i in turn (N/64 reads per lane instead of N by one lane); every lane
+    // of the wave takes part, agent or not.
+    int edgek[APL];
+#pragma unroll
+    for (int k = 0; k < APL; ++k) edgek[k] = 0;
+    if (g.L >= 64 && a.do_step && !skip) {
+      const int l64 = tid & 63;
+#pragma unroll
+      for (int k = 0; k < APL; ++k) {
+        uint64_t m = __ballot(has[k] && moved[k] && pre[k] > 0);
+        while (m) {
+          const int src = __ffsll((unsigned long long)m) - 1;
+          m &= m - 1;
+          const int tn = __shfl(nc[k], src), to = __shfl(oc[k], src);
+          int cnt = 0;
+          for (int j = l64; j < N; j += 64) cnt += (oldc[j] == tn) & (newc[j] == to);
+#pragma unroll
+          for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d);
+          if (l64 == src) edgek[k] = cnt;
+        }
+      }
+    }
 #pragma unroll
     for (int k = 0; k < APL; ++k) {
       if (!has[k]) continue;
       const int ag = lane + k * g.L;
       const long long ai = (slotE + env) * N + ag;  // output agent index
-      int node = 0, edge = 0;
+      int node = 0, edge = edgek[k];
       if (a.do_step && !skip) {
         node = ((uint32_t)map[nc[k]] & CT::CNT) > 1u ? 1 : 0;  // :344-362
-        if (moved[k] && pre[k] > 0) {                           // :364-383
+        if (g.L < 64 && moved[k] && pre[k] > 0) {
           for (int j = 0; j < N; ++j)
             edge += (oldc[j] == nc[k]) & (newc[j] == oc[k]);
         }

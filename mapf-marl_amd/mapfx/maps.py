@@ -129,3 +129,82 @@ def synthetic_instances(n_envs: int, h: int, w: int, n_agents: int, p_obstacle: 
     return {"grid": grid, "bits": pack_bits(grid), "init_pos": to_rc(starts),
             "goals": to_rc(goals)}
 
+
+
+# ---------------------------------------------------------------------------
+# PRIMAL random worlds: MAPFEnv._setWorld without a given
+# world (MARL-curve-main/src/envs/mapf_primal.py:248-341).  Host code, as in the
+# reference; it draws from the same global generators (numpy's legacy
+# np.random and the stdlib `random`) in the same order, so the same seeds give
+# the same world.
+# ---------------------------------------------------------------------------
+def _primal_region(world, memo, x, y):
+    """getConnectedRegion (:250-274): free cells 4-connected to (x, y), as a set
+    built by the reference's stack order (list(set) order then matches too).
+    Every agent cell met on the way is memoised to the same set object."""
+    if (x, y) in memo:
+        return memo[(x, y)]
+    seen = set()
+    h, w = world.shape
+    stack = [(x, y)]
+    while stack:
+        i, j = stack.pop()
+        if i < 0 or i >= h or j < 0 or j >= w or world[i, j] == -1:
+            continue
+        if world[i, j] > 0:
+            memo[(i, j)] = seen
+        if (i, j) in seen:
+            continue
+        seen.add((i, j))
+        stack.extend(((i + 1, j), (i, j + 1), (i - 1, j), (i, j - 1)))
+    memo[(x, y)] = seen
+    return seen
+
+
+def _primal_place(world, num_agents, np_random, py_random):
+    """Agents on random free cells, then each agent's goal on a random free cell of
+    its own connected region (:290-306 / :316-336).  `world` is modified in place
+    (agent ids written at the starts); returns the goals array."""
+    locs = []
+    a = 1
+    while a <= num_agents:
+        x, y = np_random.randint(0, world.shape[0]), np_random.randint(0, world.shape[1])
+        if world[x, y] == 0:
+            world[x, y] = a
+            locs.append((x, y))
+            a += 1
+    goals = np.zeros(world.shape).astype(int)
+    memo = {}
+    a = 1
+    while a <= num_agents:
+        sx, sy = locs[a - 1]
+        x, y = py_random.choice(list(_primal_region(world, memo, sx, sy)))
+        if goals[x, y] == 0 and world[x, y] != -1:
+            goals[x, y] = a
+            a += 1
+    return goals
+
+
+def primal_world(num_agents, SIZE=(10, 40), PROB=(0, .5), world0=None, blank_world=False,
+                 np_random=None, py_random=None):
+    """(world, goals) in PRIMAL's encoding (-1 obstacle, agent id at its start /
+    goal cell), as MAPFEnv(num_agents, SIZE=SIZE, PROB=PROB, world0=world0,
+    blank_world=blank_world) would set them up.
+
+    * world0 None: random square world -- obstacle density triangular over PROB,
+      side drawn from (SIZE[0], mean, SIZE[1]) with p (.5, .25, .25) (:316-318).
+    * blank_world: agents and goals placed on the given world0 (:290-306).
+    The generators default to the global np.random / random modules (the
+    reference's), so seeding those reproduces the reference's draws."""
+    import random as _random
+    npr = np.random if np_random is None else np_random
+    pyr = _random if py_random is None else py_random
+    if world0 is not None:
+        if not blank_world:
+            raise ValueError("a given world0 carries its own agents; pass blank_world=True to place them")
+        world = np.array(world0)
+        return world, _primal_place(world, num_agents, npr, pyr)
+    prob = npr.triangular(PROB[0], .33 * PROB[0] + .66 * PROB[1], PROB[1])
+    size = npr.choice([SIZE[0], SIZE[0] * .5 + SIZE[1] * .5, SIZE[1]], p=[.5, .25, .25])
+    world = -(npr.rand(int(size), int(size)) < prob).astype(int)
+    return world, _primal_place(world, num_agents, npr, pyr)

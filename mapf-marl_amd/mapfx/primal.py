@@ -17,7 +17,7 @@ import torch
 
 from . import _abi
 from ._abi import check, lib, ptr
-from .maps import map_stride, pack_bits
+from .maps import map_stride, pack_bits, primal_world
 
 _OUT_KEYS = ("reward", "done", "next_mask", "on_goal", "valid", "obs", "vec")
 
@@ -126,30 +126,52 @@ class PrimalBatch:
 
 
 class MAPFEnv:
-    """Single-world drop-in for mapf_primal.py MAPFEnv (:168-667) on the device,
-    for a given world0 / goals0 (PRIMAL's int arrays: -1 obstacle, agent id at its
-    start / goal cell).  Random world generation (_setWorld without world0, :248-341)
-    and rendering are outside the hot path."""
+    """Single-world drop-in for mapf_primal.py MAPFEnv (:168-667) on the device.
+    World set-up follows _setWorld (:248-341): a given world0 / goals0 (PRIMAL's
+    int arrays: -1 obstacle, agent id at its start / goal cell), agents and goals
+    placed on a given world (blank_world), or a random world from SIZE / PROB --
+    the last two drawn on the host by mapfx.maps.primal_world from the global
+    np.random / random generators, as the reference draws them.  Rendering is
+    outside the hot path."""
 
     def __init__(self, num_agents=1, observation_size=10, world0=None, goals0=None,
-                 DIAGONAL_MOVEMENT=False, device=None, **_unused):
-        if world0 is None or goals0 is None:
-            raise NotImplementedError("random PRIMAL worlds (_setWorld without world0) are out of scope")
+                 DIAGONAL_MOVEMENT=False, SIZE=(10, 40), PROB=(0, .5), FULL_HELP=False,
+                 blank_world=False, device=None):
         if DIAGONAL_MOVEMENT:
             raise NotImplementedError("DIAGONAL_MOVEMENT is not on the hot path")
-        world0 = np.asarray(world0)
-        goals0 = np.asarray(goals0)
         self.num_agents = int(num_agents)
         self.observation_size = int(observation_size)
+        self.SIZE, self.PROB, self.FULL_HELP = SIZE, PROB, FULL_HELP
+        self._device = device
+        self._set_world(world0, goals0, blank_world)
+
+    def _set_world(self, world0, goals0, blank_world=False):
+        if world0 is None:
+            world0, goals0 = primal_world(self.num_agents, SIZE=self.SIZE, PROB=self.PROB)
+        elif blank_world:
+            world0, goals0 = primal_world(self.num_agents, world0=world0, blank_world=True)
+        elif goals0 is None:
+            raise Exception("you gave a world with no goals!")
+        world0 = np.asarray(world0)
+        goals0 = np.asarray(goals0)
         starts, goals = [], []
         for a in range(1, self.num_agents + 1):
             starts.append(tuple(int(v) for v in np.argwhere(world0 == a)[0]))
             goals.append(tuple(int(v) for v in np.argwhere(goals0 == a)[0]))
+        self.initial_world, self.initial_goals = world0.copy(), goals0.copy()
         self._grid = np.where(world0 < 0, -1, 0).astype(np.int8)
         self.batch = PrimalBatch([starts], [goals], grids=self._grid,
-                                 observation_size=observation_size, device=device)
+                                 observation_size=self.observation_size, device=self._device)
         self.finished = False
+        self.fresh = True
         self.individual_rewards = [0 for _ in range(self.num_agents)]
+
+    def _reset(self, agent_id, world0=None, goals0=None):
+        """:389-402 -> (next valid actions, on_goal, False)."""
+        self._set_world(world0, goals0)
+        o = self.batch.act([[agent_id]], [[0]])  # a stay call changes nothing; it reports
+        mask = int(o["next_mask"][0, 0].item())  # the valid moves with no previous action
+        return [a for a in range(5) if (mask >> a) & 1], bool(o["on_goal"][0, 0].item()), False
 
     def getObstacleMap(self):
         return (self._grid == -1).astype(int)

@@ -155,3 +155,36 @@ def test_primal_rejects_bad_placement(mapfx_mod):
         mapfx_mod.PrimalBatch([[[1, 1]]], [[[0, 0]]], grids=g)
     with pytest.raises(ValueError):
         mapfx_mod.PrimalBatch([[[0, 0], [0, 0]]], [[[2, 2], [3, 3]]], grids=g)
+
+
+@pytest.mark.parametrize("name", sorted(os.path.basename(p)[:-4]
+                                        for p in glob.glob(os.path.join(GOLDEN, "pw_*.npz"))))
+def test_primal_dropin_random_world_matches_reference(mapfx_mod, name):
+    """MAPFEnv without world0 (or with blank_world) builds the reference's world for
+    the same seeds (tests/golden/pw_*.npz), then steps it on the device; _reset
+    reports the stay-free valid moves and on_goal of the new world."""
+    import random
+    from mapfx.primal import MAPFEnv
+    fx = _load(name)
+    n = int(fx["num_agents"])
+    np.random.seed(int(fx["seed"]))
+    random.seed(int(fx["seed"]))
+    if "world0" in fx:
+        env = MAPFEnv(num_agents=n, world0=fx["world0"].astype(int), blank_world=True)
+    else:
+        env = MAPFEnv(num_agents=n, SIZE=tuple(fx["SIZE"]), PROB=tuple(fx["PROB"]))
+    for a in range(1, n + 1):
+        assert env.getPositions()[a - 1] == tuple(int(v) for v in np.argwhere(fx["world"] == a)[0])
+        assert env.getGoals()[a - 1] == tuple(int(v) for v in np.argwhere(fx["goals"] == a)[0])
+    assert np.array_equal(env.getObstacleMap(), (fx["world"] == -1).astype(int))
+    world = fx["world"]
+    for a in (1, n):
+        nxt, on_goal, blocking = env._reset(a, world0=fx["world"], goals0=fx["goals"])
+        r, c = np.argwhere(world == a)[0]
+        want = [0]
+        for act, (dr, dc) in ((1, (0, 1)), (2, (1, 0)), (3, (0, -1)), (4, (-1, 0))):  # dirDict :28
+            rr, cc = r + dr, c + dc
+            if 0 <= rr < world.shape[0] and 0 <= cc < world.shape[1] and world[rr, cc] == 0:
+                want.append(act)
+        assert nxt == want and blocking is False
+        assert on_goal == (tuple(np.argwhere(fx["goals"] == a)[0]) == (r, c))

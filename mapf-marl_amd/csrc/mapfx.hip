@@ -875,11 +875,8 @@ __device__ __forceinline__ void window_regs(const uint32_t* qx, int o, uint32_t 
 #ifndef MAPFX_SPLIT_NT
 #define MAPFX_SPLIT_NT 1  // nontemporal (streaming) stores from the store wave
 #endif
-#ifndef MAPFX_SPLIT_DIRECT
-#define MAPFX_SPLIT_DIRECT 0  // 1: store wave writes window records per lane (no LDS image)
-#endif
-#ifndef MAPFX_SPLIT_DPPFOLD
-#define MAPFX_SPLIT_DPPFOLD 1  // reward fold as an in-row DPP scan (no LDS reward row)
+#ifndef MAPFX_SPLIT_WAVES
+#define MAPFX_SPLIT_WAVES 2  // 2: step + store wave; 3: step + record wave + small-output wave (slower at C2)
 #endif
 
 // `sum(rewards)` (mapf_gridworld.py:141) over a 16-lane DPP row: a naive left fold
@@ -904,11 +901,18 @@ template <int WIN, int LL>
 struct SplitLayout {
   static constexpr int REC = 2 * WIN * WIN;             // window record bytes per agent
   static constexpr int NXW = (WIN > 5 ? 3 : 2) * WIN;  // raw row words per agent
-  static constexpr int SLOT = (4 + NXW + 3) / 4 * 16;   // info u32x4 + raw rows, per agent
+  static constexpr int SLOT = (4 + NXW + 3) / 4 * 16;   // info u32x4 + raw rows, per agent,
+                                                        // stored chunk-major (bank-conflict free)
   static constexpr int BYTES = 64 * SLOT;               // one image (64 agents)
-  static constexpr int STORE_LDS = 2 * (64 * REC + 64 * 8);  // store wave: 2 x (records + reward row)
+  static constexpr int STORE_LDS = 2 * 64 * REC;       // staged-record images of the output side
   static_assert(LL == 16, "4 envs of 16 agents per wave");
 };
+#ifndef MAPFX_SPLIT_SOA
+#define MAPFX_SPLIT_SOA 1  // slot images chunk-major: chunk i of lane l at (64 i + l) * 16
+#endif
+// byte stride between lanes / u32x4 stride between one lane's chunks in a slot image
+#define SLOT_LANE (MAPFX_SPLIT_SOA ? 16 : SplitLayout<WIN, LL>::SLOT)
+#define SLOT_CHUNK (MAPFX_SPLIT_SOA ? 64 : 1)
 
 // info.z flag bits
 constexpr uint32_t SF_DONE = 1, SF_LIVE = 2, SF_DNOLD = 4, SF_ENVC = 8, SF_SKIP = 16, SF_OBST = 32,
@@ -933,65 +937,49 @@ __device__ __forceinline__ int2 padded_cell_rc(const Geo& g, int cell) {
   return make_int2((int)pr - g.P, cell - (int)pr * g.pitch - g.pl);
 }
 
-// Store wave, software-pipelined by one step: after the barrier that hands over
-// step q's image it issues, together, the reads of that image and of its own
-// LDS images of step q-1 (staged window records, per-agent reward row); then it
-// writes step q-1's records and folds step q-1's reward while deriving step q's
-// outputs, so each step costs it one LDS round trip.
-template <int WIN, int LL>
+// Output side of the split.  ROLE_ALL: one store wave does everything (2-wave
+// workgroups); with MAPFX_SPLIT_WAVES == 3 a "record wave" (ROLE_REC: window
+// records) and a "small wave" (ROLE_SMALL: node / edge / avail / done / (row, col),
+// fp64 reward fold, t, term) share the work.  Both read the step wave's image
+// after the barrier that hands it over.
+//   records: SWAR planes from the raw rows, staged in the wave's own LDS image
+//     and written one step later with lane-contiguous 16-byte stores (the
+//     staged step q-1 is read together with step q's image: one LDS round trip
+//     per step);
+//   small outputs: derived from the info word and the centre row; the reward
+//     fold is an in-row DPP scan (row_fold16), lane LL-1 of each env stores it.
+constexpr int ROLE_ALL = 0, ROLE_REC = 1, ROLE_SMALL = 2;
+
+template <int WIN, int LL, int ROLE>
 __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, unsigned char* sp,
-                                                 int env0, int lane) {
+                                                 unsigned char* own, int env0, int lane) {
   typedef __attribute__((address_space(1))) unsigned char gbyte;  // global_store, not flat_
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   typedef int i32x2 __attribute__((ext_vector_type(2)));
   using SL = SplitLayout<WIN, LL>;
+  constexpr bool RECS = ROLE != ROLE_SMALL, SMALL = ROLE != ROLE_REC;
   constexpr int H2 = WIN / 2, REC = SL::REC, NQ = SL::SLOT / 16;
   constexpr int RCH = 4 * REC;                  // 16-byte chunks of the wave's 64 records
   constexpr int NRC = (RCH + 63) / 64;          // chunk rounds per lane
-  constexpr int IMG = SL::STORE_LDS / 2;        // one store-wave image: records + reward row
-  constexpr bool DIRECT = MAPFX_SPLIT_DIRECT;   // records straight from registers (no image)
-  constexpr bool DPPFOLD = MAPFX_SPLIT_DPPFOLD;  // fold as an in-row DPP scan, same step
+  constexpr int IMG = 64 * REC;                 // one staged-record image
   const int T = a.T;
   const uint32_t E = (uint32_t)g.E, EN = E * (uint32_t)LL;
   const int slot = lane / LL, ag = lane % LL;
   const uint32_t env = (uint32_t)(env0 + slot), ag0 = (uint32_t)env0 * LL;
-  unsigned char* own = sp + 2 * g.wv_split_buf;  // 2 images of [64 * REC records | 64 doubles]
+  const u32x4* ost = (const u32x4*)__builtin_assume_aligned(own, 16);
 
-  // step p's staged records and reward row (image p & 1) -> HBM; env outputs of p
-  uint32_t p_fl = 0;
-  int p_tcur = 0;
-  auto finish = [&](uint32_t p, const u32x4 (&rv)[NRC], const double (&v)[LL], bool ok) {
-    gbyte* rec = (gbyte*)a.obs_window + (p * EN + ag0) * (uint32_t)REC;
-    if constexpr (!DIRECT) {
+  // staged records of step p (image p & 1): read / store
+  auto read_recs = [&](uint32_t p, u32x4 (&rv)[NRC]) {
 #pragma unroll
-      for (int k = 0; k < NRC; ++k)
-        if (ok && (k < NRC - 1 || lane + 64 * k < RCH))
-          split_store((__attribute__((address_space(1))) u32x4*)(rec + 16u * (lane + 64 * k)), rv[k]);
-    }
-    // `sum(rewards)` (:141): naive left fold in agent order -- in every lane, so the
-    // dependent adds share a basic block with (and interleave into) the next step's work
-    double Rs = 0.0;
-#pragma unroll
-    for (int j = 0; j < LL; ++j) Rs = Rs + v[j];
-    if (!DPPFOLD && ok && ag == 0) {
-      const uint32_t ei = p * E + env;
-      split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), Rs);
-      split_store((__attribute__((address_space(1))) int*)((gbyte*)a.traj_t + 4u * ei), p_tcur);
-      split_store((gbyte*)a.term + ei, (unsigned char)((p_fl & SF_ALLDONE) ? 1 : 0));
-      if (a.reward_f32) a.reward_f32[ei] = (float)Rs;
-      if (a.err && (p_fl & SF_SKIP)) atomicCAS(a.err, 0, (int)env + 1);
-    }
+    for (int k = 0; k < NRC; ++k)
+      rv[k] = ost[(p & 1) * (IMG / 16) + ((k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0)];
   };
-  auto read_own = [&](uint32_t p, u32x4 (&rv)[NRC], double (&v)[LL]) {
-    const unsigned char* im = own + (p & 1) * IMG;
-    const u32x4* st = (const u32x4*)__builtin_assume_aligned(im, 16);
-    if constexpr (!DIRECT) {
+  auto store_recs = [&](uint32_t p, const u32x4 (&rv)[NRC], bool ok) {
+    gbyte* rec = (gbyte*)a.obs_window + (p * EN + ag0) * (uint32_t)REC;
 #pragma unroll
-      for (int k = 0; k < NRC; ++k) rv[k] = st[(k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0];
-    }
-    const double* r = (const double*)(im + 64 * REC) + slot * LL;
-#pragma unroll
-    for (int j = 0; j < LL; ++j) v[j] = DPPFOLD ? 0.0 : r[j];
+    for (int k = 0; k < NRC; ++k)
+      if (ok && (k < NRC - 1 || lane + 64 * k < RCH))
+        split_store((__attribute__((address_space(1))) u32x4*)(rec + 16u * (lane + 64 * k)), rv[k]);
   };
 
   const int rounds = T > 0 ? T + 1 : 0;
@@ -1000,46 +988,56 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
     if (s == 1 || (MAPFX_ABLATE & 256)) continue;
     const uint32_t q = (uint32_t)(s - 2);  // the step image (s - 1) & 1 carries
     const u32x4* sl = (const u32x4*)__builtin_assume_aligned(
-        sp + ((s - 1) & 1) * g.wv_split_buf + lane * SL::SLOT, 16);
+        sp + ((s - 1) & 1) * g.wv_split_buf + lane * SLOT_LANE, 16);
     uint32_t w[4 * NQ];
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
-      const u32x4 v = sl[i];
+      const u32x4 v = sl[SLOT_CHUNK * i];
       w[4 * i] = v.x;
       w[4 * i + 1] = v.y;
       w[4 * i + 2] = v.z;
       w[4 * i + 3] = v.w;
     }
     u32x4 rv[NRC];
-    double pv[LL];
-    read_own(q - 1, rv, pv);  // q = 0: stale image, nothing of it is stored
+    if constexpr (RECS) read_recs(q - 1, rv);  // q = 0: stale image, nothing of it is stored
     const int nc = (int)w[0];
     const uint32_t nb = w[1], fl = w[2];
     const uint32_t* qx = w + 4;
     const int o = (nc - H2) & 3;
-    uint32_t R[4 * WIN];
-    window_regs<WIN>(qx, o, R);
-    // node collision (:344-362): post-step count = c - 1 + obstacle >= 2 (centre cell)
-    const uint32_t ctr = (__builtin_amdgcn_alignbyte(qx[WIN + H2], qx[H2], o) >> (8 * H2)) & 0xFFu;
-    uint32_t node = ctr + ((fl / SF_OBST) & 1u) >= 3u ? 1u : 0u;
-    if (fl & SF_SKIP) node = 0;
-    // avail (:203-224): a neighbour is available iff its c != 0; stay always
-    const uint32_t nzn = ((nb + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
-    const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
-    const uint32_t edge = fl >> 8;
-    // reward (:94-130, exact fp64 op order)
-    double rr = 0.0;
-    if (fl & SF_LIVE) {
-      if (!(fl & SF_DNOLD)) {
-        if (fl & SF_ENVC) rr = rr + g.collide_rew;
-        rr = rr + g.step_rew;
-      }
-      rr = rr + g.collide_rew * (double)node;
-      rr = rr + g.collide_rew * (double)edge;
+    if constexpr (RECS) {
+      uint32_t R[4 * WIN];
+      window_regs<WIN>(qx, o, R);
+      store_recs(q - 1, rv, q > 0);
+      stage_record<WIN>(R, own + (q & 1) * IMG + lane * REC);
     }
-    finish(q - 1, rv, pv, q > 0);
-    if constexpr (DPPFOLD) {  // `sum(rewards)` (:141); lane LL-1 of the env holds the total
-      const double Rs = row_fold16(rr);
+    if constexpr (SMALL) {
+      // node collision (:344-362): post-step count = c - 1 + obstacle >= 2 (centre cell)
+      const uint32_t ctr = (__builtin_amdgcn_alignbyte(qx[WIN + H2], qx[H2], o) >> (8 * H2)) & 0xFFu;
+      uint32_t node = ctr + ((fl / SF_OBST) & 1u) >= 3u ? 1u : 0u;
+      if (fl & SF_SKIP) node = 0;
+      // avail (:203-224): a neighbour is available iff its c != 0; stay always
+      const uint32_t nzn = ((nb + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
+      const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
+      const uint32_t edge = fl >> 8;
+      // reward (:94-130, exact fp64 op order)
+      double rr = 0.0;
+      if (fl & SF_LIVE) {
+        if (!(fl & SF_DNOLD)) {
+          if (fl & SF_ENVC) rr = rr + g.collide_rew;
+          rr = rr + g.step_rew;
+        }
+        rr = rr + g.collide_rew * (double)node;
+        rr = rr + g.collide_rew * (double)edge;
+      }
+      const uint32_t ai = q * EN + ag0 + lane;
+      const int2 rc = padded_cell_rc(g, nc);
+      split_store((__attribute__((address_space(1))) i32x2*)((gbyte*)a.traj_pos + 8u * ai),
+                  i32x2{rc.x, rc.y});
+      split_store((gbyte*)a.node + ai, (unsigned char)node);
+      split_store((gbyte*)a.edge + ai, (unsigned char)edge);
+      split_store((gbyte*)a.avail + ai, (unsigned char)availm);
+      split_store((gbyte*)a.traj_done + ai, (unsigned char)(fl & SF_DONE));
+      const double Rs = row_fold16(rr);  // `sum(rewards)` (:141): lane LL-1 holds the total
       if (ag == LL - 1) {
         const uint32_t ei = q * E + env;
         split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), Rs);
@@ -1049,27 +1047,14 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
         if (a.err && (fl & SF_SKIP)) atomicCAS(a.err, 0, (int)env + 1);
       }
     }
-    unsigned char* im = own + (q & 1) * IMG;
-    const uint32_t ai = q * EN + ag0 + lane;
-    if constexpr (DIRECT) write_record<WIN>(R, a.obs_window, ai * (uint32_t)REC);
-    else stage_record<WIN>(R, im + lane * REC);
-    ((double*)(im + 64 * REC))[lane] = rr;
-    const int2 rc = padded_cell_rc(g, nc);
-    split_store((__attribute__((address_space(1))) i32x2*)((gbyte*)a.traj_pos + 8u * ai),
-                i32x2{rc.x, rc.y});
-    split_store((gbyte*)a.node + ai, (unsigned char)node);
-    split_store((gbyte*)a.edge + ai, (unsigned char)edge);
-    split_store((gbyte*)a.avail + ai, (unsigned char)availm);
-    split_store((gbyte*)a.traj_done + ai, (unsigned char)(fl & SF_DONE));
-    p_fl = fl;
-    p_tcur = (int)w[3];
   }
-  if (T > 0 && !(MAPFX_ABLATE & 256)) {  // the last step's records and reward
-    wave_fence();
-    u32x4 rv[NRC];
-    double pv[LL];
-    read_own((uint32_t)(T - 1), rv, pv);
-    finish((uint32_t)(T - 1), rv, pv, true);
+  if constexpr (RECS) {
+    if (T > 0 && !(MAPFX_ABLATE & 256)) {  // the last step's staged records
+      wave_fence();
+      u32x4 rv[NRC];
+      read_recs((uint32_t)(T - 1), rv);
+      store_recs((uint32_t)(T - 1), rv, true);
+    }
   }
 }
 
@@ -1090,13 +1075,17 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
 // so only A and D (a few dozen instructions) sit on the serial chain between
 // steps.  The last step's heavy part and tails run after the loop.
 template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false>
-__global__ void __launch_bounds__(SPLIT ? 128 : 64) mapf_wave_kernel(Geo g, Args a) {
+__global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave_kernel(Geo g, Args a) {
   extern __shared__ __align__(16) unsigned char lds[];
   static_assert(!SPLIT || (ROLL && FULLW && RUNNER && LL == 16 && WIN > 0), "split: runner rollout, N = 16");
   if constexpr (SPLIT) {
     if (threadIdx.x >= 64) {  // the output side of the split
       const int e0 = xcd_block(blockIdx.x, gridDim.x) * (64 / LL);
-      split_store_wave<WIN, LL>(g, a, lds + g.wv_off_split, e0, threadIdx.x & 63);
+      unsigned char* sp = lds + g.wv_off_split;
+      unsigned char* own = sp + 2 * g.wv_split_buf;
+      if (MAPFX_SPLIT_WAVES == 2) split_store_wave<WIN, LL, ROLE_ALL>(g, a, sp, own, e0, threadIdx.x & 63);
+      else if (threadIdx.x < 128) split_store_wave<WIN, LL, ROLE_REC>(g, a, sp, own, e0, threadIdx.x & 63);
+      else split_store_wave<WIN, LL, ROLE_SMALL>(g, a, sp, own, e0, threadIdx.x & 63);
       return;
     }
   }
@@ -1279,7 +1268,7 @@ __global__ void __launch_bounds__(SPLIT ? 128 : 64) mapf_wave_kernel(Geo g, Args
       using SL = SplitLayout<WIN, LL>;
       const int edge = edge_of();
       u32x4* sl = (u32x4*)__builtin_assume_aligned(
-          lds + g.wv_off_split + ((qs + 1) & 1) * g.wv_split_buf + lane64 * SL::SLOT, 16);
+          lds + g.wv_off_split + ((qs + 1) & 1) * g.wv_split_buf + lane64 * SLOT_LANE, 16);
       const uint32_t fl = (q_dn ? SF_DONE : 0u) | (q_live ? SF_LIVE : 0u) | (q_dnold ? SF_DNOLD : 0u) |
                           (q_envc ? SF_ENVC : 0u) | (q_skip ? SF_SKIP : 0u) | ((q_dj >> 7) ? SF_OBST : 0u) |
                           (q_alldone ? SF_ALLDONE : 0u) | ((uint32_t)(edge > 255 ? 255 : edge) << 8);
@@ -1293,7 +1282,8 @@ __global__ void __launch_bounds__(SPLIT ? 128 : 64) mapf_wave_kernel(Geo g, Args
 #pragma unroll
       for (int i = 4 + SL::NXW; i < SL::SLOT / 4; ++i) w[i] = 0;
 #pragma unroll
-      for (int i = 0; i < SL::SLOT / 16; ++i) sl[i] = u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+      for (int i = 0; i < SL::SLOT / 16; ++i)  // chunk-major: lanes write consecutive 16-B chunks
+        sl[SLOT_CHUNK * i] = u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
       return;
     }
     const uint32_t so = ROLL ? (uint32_t)qs * EN : 0u;
@@ -1721,13 +1711,13 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream) {
     const uintptr_t al16 = (uintptr_t)a.obs_window | (uintptr_t)a.traj_pos | (uintptr_t)a.node |
                            (uintptr_t)a.edge | (uintptr_t)a.avail | (uintptr_t)a.traj_done |
                            (uintptr_t)a.reward | (uintptr_t)a.traj_t;
-    const int split_lds = g.wv_lds + 2 * g.wv_split_buf + 2 * (64 * g.wlen + 64 * 8);  // + store-wave images
+    const int split_lds = g.wv_lds + 2 * g.wv_split_buf + 2 * 64 * g.wlen;  // + staged-record images
     const bool split = MAPFX_SPLIT && runner && fullw && g.L == 16 && g.wv_split_buf > 0 &&
                        split_lds <= 64 * 1024 && (al16 & 15) == 0;
     KernelFn fn = pick_wave_kernel(a.obs_window ? g.window : 0, roll, fullw, runner, g.L, split);
     if (fn) {
       const int blocks = (g.E + g.EPW - 1) / g.EPW;
-      hipLaunchKernelGGL(fn, dim3(blocks), dim3(split ? 128 : 64),
+      hipLaunchKernelGGL(fn, dim3(blocks), dim3(split ? 64 * MAPFX_SPLIT_WAVES : 64),
                          split ? split_lds : g.wv_lds, stream, g, a);
       return check_hip(hipGetLastError(), "mapf_wave_kernel launch");
     }

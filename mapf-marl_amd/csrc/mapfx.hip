@@ -1421,7 +1421,10 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
     const int nc = moved ? oc + dlt : oc;
     if (has && !(MAPFX_ABLATE & 64)) dep[oc] = (unsigned char)((f_cur << 7) | (moved ? (uint32_t)act : 0x7Fu));
     if (!(MAPFX_ABLATE & 16)) {
-      if (FULLW) {  // branch-free: lanes that stay add 0 to their own cell's word
+#ifndef MAPFX_FULLW_ATOMICS
+#define MAPFX_FULLW_ATOMICS 1
+#endif
+      if (FULLW && MAPFX_FULLW_ATOMICS) {  // branch-free: lanes that stay add 0 to their own cell's word
         atomicAdd(&map32[oc >> 2], moved ? 0u - (1u << ((oc & 3) * 8)) : 0u);
         atomicAdd(&map32[nc >> 2], moved ? 1u << ((nc & 3) * 8) : 0u);
       } else if (moved) {

@@ -322,7 +322,7 @@ int orc_rollout(const orc_cfg* c, int32_t T, uint64_t seed, int32_t t0, int32_t*
                  reward ? reward + e : NULL, node ? node + e * N : NULL,
                  edge ? edge + e * N : NULL, occ, newp, rew, cnt);
         observe_env(c, pos + e * 2 * N, goal + e * 2 * N, done + e * N, env_bits(c, bits, e), occ,
-                    avail ? avail + e * N : NULL, NULL, NULL, 0,
+                    avail ? avail + e * N : NULL, NULL, NULL, es == 2,
                     obs_window ? (char*)obs_window + e * (int64_t)N * 2 * window * window * es
                                : NULL,
                     window, NULL, NULL, 0, NULL);

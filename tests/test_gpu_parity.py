@@ -272,6 +272,36 @@ def test_rollout_matches_oracle_long_horizon(mapfx_mod):
     assert np.array_equal(_np(traj["obs_window"][-1]), ref["obs_window"])
 
 
+
+@pytest.mark.parametrize("name,E,S,N,T,shared", [
+    ("c3_full_2048x64_warehouse", 2048, 64, 64, 32, True),
+    ("c5_full_1024x256", 1024, 128, 256, 16, False)])
+def test_rollout_matches_oracle_full_size(mapfx_mod, name, E, S, N, T, shared):
+    """BASELINE C3 and C5 at their full env counts: a fused
+    generator-action rollout equals the C oracle's, every env, bit for bit."""
+    from oracle import corc
+    inst = _instances(mapfx_mod, E, S, N, 0.10, shared, seed=1)
+    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                                episode_limit=2000, obs=("window",))
+    ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=2000)
+    b.reset()
+    traj = b.rollout(T, seed=2, t0=0)
+    ref = ob.rollout(T, seed=2, t0=0)
+    assert np.array_equal(_np(b.pos), ob.pos), name
+    assert np.array_equal(_np(b.done), ob.done), name
+    assert np.array_equal(_np(b.t), ob.t), name
+    assert np.array_equal(_u64(_np(traj["reward"][-1])), _u64(ref["reward"])), name
+    assert np.array_equal(_np(traj["node"][-1]), ref["node"]), name
+    assert np.array_equal(_np(traj["edge"][-1]), ref["edge"]), name
+    assert np.array_equal(_np(traj["avail"][-1]), ref["avail"]), name
+    assert np.array_equal(_np(traj["obs_window"][-1]), ref["obs_window"]), name
+    # size-independent: every agent stays in bounds and the window's agent plane
+    # counts each agent's own cell (>= 1)
+    pos = _np(b.pos)
+    assert pos.min() >= 0 and pos.max() < S
+    assert (_np(traj["obs_window"][-1])[:, :, 1, 2, 2] >= 1).all()
+
+
 def test_autoreset(mapfx_mod):
     """Envs whose agents are all done restart from init_pos in the fused rollout,
     identically to step + reset(mask)."""

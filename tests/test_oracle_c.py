@@ -106,3 +106,22 @@ def test_c_oracle_rejects_bad_actions():
     a = np.array([[0, 1, 2, 3, 4, 5, 0, 1]], np.int32)
     assert ob.step(a)["bad"] == 1
     assert np.array_equal(ob.pos, pos0) and ob.t[0] == 0
+
+
+@pytest.mark.parametrize("N", [16, 200])
+def test_c_oracle_rollout_window_equals_observe(N):
+    """orc_rollout's last-step window equals orc_observe on the final state,
+    including the int16 layout used when N > 127."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "mapf-marl_amd"))
+    from mapfx.maps import synthetic_instances
+    S, E, T = 24, 4, 6
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.05, seed=1)
+    ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=2000,
+                          nthreads=2)
+    r = ob.rollout(T, seed=2)
+    o = ob.observe()
+    assert r["obs_window"].dtype == (np.int16 if N > 127 else np.int8)
+    assert np.array_equal(r["obs_window"], o["obs_window"])
+    assert np.array_equal(r["avail"], o["avail"])

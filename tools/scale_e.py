@@ -21,12 +21,13 @@ def main():
     ap.add_argument("--launches", type=int, default=6)
     ap.add_argument("--envs", default="256,1024,2048,4096,8192,16384,32768")
     ap.add_argument("--n", type=int, default=16)
+    ap.add_argument("--S", type=int, default=32, help="grid side (C5: 128)")
     ap.add_argument("--Ts", default="", help="comma list of T at E=4096 instead of the E sweep")
     ap.add_argument("--rng", action="store_true", help="device-generated actions (no action loads)")
     a = ap.parse_args()
     import mapfx
     from mapfx.maps import synthetic_instances
-    S, N, T = 32, a.n, a.T
+    S, N, T = a.S, a.n, a.T
     outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done",
             "traj_t")
     runs = [(int(x), T) for x in a.envs.split(",")]

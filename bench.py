@@ -57,7 +57,7 @@ def parse():
                     help="target CPU work of the cpu_baseline sample (0 disables)")
     ap.add_argument("--gather", action="store_true",
                     help="also time the RCCL gather of (obs, reward, done) to rank 0")
-    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_c2.json"))
+    ap.add_argument("--pmc", default=None, help="PMC summary (default profiles/pmc_<config>.json)")
     ap.add_argument("--env", default="mapf_grid", choices=("mapf_grid", "marl_partial", "runner"),
                     help="mapf_grid: the BASELINE.json metric (default); marl_partial: the "
                          "SURVEY §8(f) F1 env on its yaml config, one launch per step")
@@ -221,7 +221,7 @@ def main():
 
     traffic = None
     try:
-        with open(args.pmc) as f:
+        with open(args.pmc or os.path.join(REPO, "profiles", "pmc_%s.json" % args.config)) as f:
             pm = json.load(f)
         if pm.get("config") == args.config and pm.get("T") == T and pm.get("E") == E:
             traffic = pm.get("traffic_bytes_per_launch")

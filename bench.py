@@ -14,8 +14,15 @@ fused rollout kernel (`mapfx_rollout`, T steps per launch, state kept on
 chip); the per-step drop-in path (`mapfx_step`, one launch per step, state
 round-trips HBM) is measured too and reported under "per_step".
 
+The timed K env steps run as launches of T = min(K, --chunk) fused steps (one
+launch of T = 20 at the driver's --steps 20), every launch prepared before the
+timed region so it holds only the foreign calls.
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+With --gpus N > 1 and no torchrun environment, bench.py starts the N rank
+processes itself (launch_ranks) and refuses to run when fewer than N HIP devices
+are visible.  `--dist-selftest` rehearses that multi-rank path on CPU (gloo).
 """
 from __future__ import annotations
 
@@ -55,8 +62,11 @@ def parse():
     ap.add_argument("--per-step-steps", type=int, default=200)
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU work of the cpu_baseline sample (0 disables)")
-    ap.add_argument("--gather", action="store_true",
-                    help="also time the RCCL gather of (obs, reward, done) to rank 0")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N > 1: skip the RCCL gather leg (reported beside the compute-only value)")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="CPU/gloo rehearsal of the multi-rank launch + shard + packed gather")
+    ap.add_argument("--selftest-envs", type=int, default=6)
     ap.add_argument("--pmc", default=None, help="PMC summary (default profiles/pmc_<config>.json)")
     ap.add_argument("--env", default="mapf_grid", choices=("mapf_grid", "marl_partial", "runner"),
                     help="mapf_grid: the BASELINE.json metric (default); marl_partial: the "
@@ -79,11 +89,109 @@ def canonical_bytes_per_env_step(H, Wd, N, W):
         + 2 * W * W * N
 
 
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, need_gpus=True):
+    """`bench.py --gpus N` without torchrun: start N rank processes of this script
+    (one per GPU, torchrun's RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* environment)
+    as children, wait for all of them and return the worst exit code.  The parent
+    never touches the GPU (it only counts devices) and never exec()s."""
+    import subprocess
+    if need_gpus:
+        have = torch.cuda.device_count()
+        if have < n:
+            print("bench.py: --gpus %d requested but only %d HIP device(s) visible; refusing "
+                  "to report a %d-rank result" % (n, have, n), file=sys.stderr, flush=True)
+            return 2
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0:
+                rc = rc or (code if code > 0 else 1)
+                for q in pending:          # a failed rank would leave the others blocked
+                    q.terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def dist_selftest(args, rank, world):
+    """CPU (gloo) rehearsal of the multi-rank bench plumbing: each rank builds the
+    weak-scaling shard bench.py would give it (global env ids [rank*E, (rank+1)*E)),
+    packs its (obs-shaped, reward, done) inputs into one ChunkLayout buffer and rank 0
+    gathers them with ONE gather.  Rank 0 checks the result against an unsharded
+    build of all world*E envs and prints one JSON line."""
+    import torch.distributed as dist
+    from mapfx.dist import ChunkLayout
+    from mapfx.maps import synthetic_instances
+    dist.init_process_group("gloo")
+    S, N, E = 16, 8, args.selftest_envs
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=1, env_offset=rank * E)
+    spec = {"init_pos": ((E, N, 2), torch.int32), "goals": ((E, N, 2), torch.int32),
+            "bits": (inst["bits"].shape, torch.uint8), "rank": ((1,), torch.int64)}
+    lay = ChunkLayout(spec, order=("init_pos", "goals", "bits", "rank"))
+    flat = lay.alloc("cpu")
+    v = lay.views(flat)
+    v["init_pos"].copy_(torch.from_numpy(inst["init_pos"]))
+    v["goals"].copy_(torch.from_numpy(inst["goals"]))
+    v["bits"].copy_(torch.from_numpy(inst["bits"]))
+    v["rank"].fill_(rank)
+    recv = torch.empty((world, lay.nbytes), dtype=torch.uint8) if rank == 0 else None
+    dist.gather(flat, gather_list=list(recv.unbind(0)) if rank == 0 else None, dst=0)
+    if rank == 0:
+        g = lay.views(recv)
+        full = synthetic_instances(world * E, S, S, N, p_obstacle=0.1, seed=1)
+        ok = (g["rank"].view(-1).tolist() == list(range(world))
+              and all(np.array_equal(g[k].reshape((world * E,) + g[k].shape[2:]).numpy(), full[k])
+                      for k in ("init_pos", "goals", "bits")))
+        print(json.dumps({"dist_selftest": "ok" if ok else "MISMATCH", "n_gpus": world,
+                          "world": world, "envs_per_rank": E, "backend": "gloo",
+                          "launcher": "torchrun env" if os.environ.get("TORCHELASTIC_RUN_ID")
+                          else "bench.py launch_ranks"}), flush=True)
+        rc = 0 if ok else 3
+    else:
+        rc = 0
+    dist.barrier()
+    dist.destroy_process_group()
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], need_gpus=not args.dist_selftest))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr)
+        sys.exit(2)
+    if args.dist_selftest:
+        sys.exit(dist_selftest(args, rank, world))
+    if torch.cuda.device_count() <= local:
+        print("bench.py: rank %d needs HIP device %d, %d visible" % (rank, local,
+              torch.cuda.device_count()), file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -99,9 +207,10 @@ def main():
         return run_runner(args, dist, rank, world, local)
     S, N, E, p, shared = CONFIGS[args.config]
     W = args.window
-    K, WU, T = args.steps, args.warmup, args.chunk
-    if K % T or WU % T:
-        T = int(np.gcd(K, max(WU, T)) or 1)
+    K, WU = args.steps, args.warmup
+    T = max(1, min(K, args.chunk))          # env steps per rollout launch
+    n_full, rem = divmod(K, T)              # K = n_full launches of T (+ one of rem)
+    n_wu = -(-WU // T) if WU > 0 else 0     # warmup: whole launches of the timed shape
     offset = rank * E                 # weak scaling: rank r owns global envs [r*E, (r+1)*E)
     inst = synthetic_instances(E, S, S, N, p_obstacle=p or 0.0, seed=1, env_offset=offset,
                                shared_grid=warehouse_grid(S) if shared else None)
@@ -111,38 +220,45 @@ def main():
                             device="cuda:%d" % local, env_offset=offset, track_steps=False)
     b.reset()
     stream = torch.cuda.current_stream()
-    acts = b.gen_actions(WU + K, seed=2)                       # inputs resident in HBM
+    acts = b.gen_actions(n_wu * T + K, seed=2)                 # inputs resident in HBM
     traj = b._alloc_out(T)
     traj.pop("reward_f32")
     outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done",
             "traj_t")
 
-    def run_chunk(k0):
-        b.rollout(T, actions=acts[k0:k0 + T], traj=traj, outputs=outs)
+    def plan(k0, t):
+        tr = traj if t == T else {k: v[:t] for k, v in traj.items()}
+        return b.rollout_plan(t, actions=acts[k0:k0 + t], traj=tr, outputs=outs, stream=stream)
 
-    # ---- warmup ----
-    for k0 in range(0, WU, T):
-        run_chunk(k0)
+    # ---- warmup: whole launches of the timed shape (>= W env steps) ----
+    for i in range(n_wu):
+        plan(i * T, T)()
     torch.cuda.synchronize()
+    # every timed launch prepared up front: the timed region is ctypes calls only
+    k0 = n_wu * T
+    plans = [plan(k0 + i * T, T) for i in range(n_full)]
+    if rem:
+        plans.append(plan(k0 + n_full * T, rem))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)       # torch creates the HIP events at their first record():
+    e1.record(stream)       # do that here, not inside the timed region
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
 
     # ---- timed: exactly K env steps of all envs ----
-    nl = K // T
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(nl)]
     t0 = time.perf_counter()
-    for i in range(nl):
-        ev[i][0].record(stream)
-        run_chunk(WU + i * T)
-        ev[i][1].record(stream)
+    e0.record(stream)
+    for pl in plans:
+        pl()
+    e1.record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    kern_ms = float(np.mean([a.elapsed_time(c) for a, c in ev]))
+    kern_ms_total = e0.elapsed_time(e1)         # HIP events on the launch stream
+    kern_ms = kern_ms_total / len(plans)
     el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if dist:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -153,8 +269,9 @@ def main():
     bpes = out_bytes_per_env_step(N, W)
     state_io = E * ((8 + 8 + 1) * N + 4 + inst["bits"].shape[1] * (0 if shared else 1)
                     + (8 + 1) * N + 4)             # per-launch state read + write-back
-    launch_bytes = E * T * bpes + state_io
-    achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
+    timed_bytes = E * K * bpes + len(plans) * state_io
+    launch_bytes = timed_bytes / len(plans)
+    achieved = timed_bytes / (kern_ms_total * 1e-3) / 1e9
 
     # ---- per-step path (one mapfx_step launch per env step) ----
     # `ks` launches captured once as a HIP graph and replayed: kernels back to back,
@@ -167,18 +284,19 @@ def main():
                                  device="cuda:%d" % local, env_offset=offset, track_steps=False)
         b2.reset()
         ks = args.per_step_steps
+        na = acts.shape[0]
         pouts = ("reward", "term", "node", "edge", "avail", "obs_window")
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for k in range(ks):
-                b2.step(acts[k % (WU + K)], outputs=pouts)
+                b2.step(acts[k % na], outputs=pouts)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             for k in range(ks):
-                b2.step(acts[k % (WU + K)], outputs=pouts)
+                b2.step(acts[k % na], outputs=pouts)
         graph.replay()
         torch.cuda.synchronize()
         pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -193,7 +311,7 @@ def main():
         pk_ms = pe0.elapsed_time(pe1) / (reps * ks)
         t2 = time.perf_counter()
         for k in range(ks):
-            b2.step(acts[k % (WU + K)], outputs=pouts)
+            b2.step(acts[k % na], outputs=pouts)
         torch.cuda.synchronize()
         eager_ms = (time.perf_counter() - t2) / ks * 1e3
         cb = canonical_bytes_per_env_step(S, S, N, W)
@@ -209,22 +327,27 @@ def main():
                          "bytes_per_env_step": cb},
         }
 
-    # ---- optional RCCL gather of (obs, reward, done) to rank 0 ----
+    # ---- RCCL gather of (obs, reward, done) to rank 0 (N > 1: on by default) ----
     gather = None
-    if dist and args.gather:
-        gather = time_gather(dist, b, acts, outs, T, WU, K, world, E, N)
+    if dist and not args.no_gather:
+        gather = time_gather(dist, b, acts, outs, T, n_wu * T, K, world, E, N)
 
     # ---- CPU baseline: the oracle's C restatement on this host (rank 0, N=1) ----
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(inst, S, N, E, W, args.cpu_seconds)
 
-    traffic = None
+    traffic, traffic_src = None, None
+    pmc_path = args.pmc or os.path.join(REPO, "profiles", "pmc_%s.json" % args.config)
     try:
-        with open(args.pmc or os.path.join(REPO, "profiles", "pmc_%s.json" % args.config)) as f:
+        with open(pmc_path) as f:
             pm = json.load(f)
-        if pm.get("config") == args.config and pm.get("T") == T and pm.get("E") == E:
-            traffic = pm.get("traffic_bytes_per_launch")
+        if pm.get("config") == args.config and pm.get("T") == T and pm.get("E") == E \
+                and pm.get("traffic_bytes_per_launch"):
+            traffic = pm["traffic_bytes_per_launch"]
+            traffic_src = "%s: %s" % (os.path.relpath(pmc_path, REPO),
+                                      pm.get("command", "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                                        "passes at T=%d" % T))
     except (OSError, ValueError):
         pass
 
@@ -243,16 +366,24 @@ def main():
             "dtype": "int32+f64",
             "data": "synthetic (splitmix64 random maps p=%.2f, distinct free starts/goals, "
                     "uniform random actions in HBM)" % (p or 0.0),
-            "config": {"workload": "%s: %dx%d grid, %d agents, %d envs/GPU, window %dx%d obs, "
-                                   "fused rollout T=%d" % (args.config, S, S, N, E, W, W, T),
-                       "envs_total": total_envs, "agents": N, "grid": [S, S],
+            "config": {"workload": "%s: %dx%d %s, %d agents, %d envs/GPU, window %dx%d obs, "
+                                   "fused rollout T=%d env-steps per launch (%d launch%s)"
+                                   % (args.config, S, S, "square synthetic warehouse (shelf "
+                                      "blocks, stands in for highway_layout_v19)" if shared
+                                      else "grid", N, E, W, W, T, len(plans),
+                                      "" if len(plans) == 1 else "es"),
+                       "envs_total": total_envs, "agents": N, "grid": [S, S], "chunk_T": T,
                        "parallelism": "env-shard x%d" % world},
             "env_steps_per_s": round(total_envs * K / elapsed, 1),
             "kernel_ms_per_launch": round(kern_ms, 5),
+            "timing": {"wall_ms": round(elapsed * 1e3, 4),
+                       "kernel_ms_events": round(kern_ms_total, 4),
+                       "launches": len(plans),
+                       "wall_over_kernel": round(elapsed * 1e3 / kern_ms_total, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "bytes_per_env_step": bpes,
-                         "bytes_per_launch": int(launch_bytes)},
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "bytes_per_env_step": bpes, "bytes_per_launch": int(launch_bytes)},
             "per_step": per_step,
             "cpu_baseline": cpu,
         }
@@ -264,27 +395,35 @@ def main():
         dist.destroy_process_group()
 
 
-def time_gather(dist, b, acts, outs, T, WU, K, world, E, N):
-    """Rollout chunks with each chunk's (window obs, reward, done) gathered to rank 0
-    over RCCL on a side stream, overlapped with the next chunk (mapfx.dist)."""
+def time_gather(dist, b, acts, outs, T, k0, K, world, E, N):
+    """The same K env steps as rollout chunks of T, each chunk's (window obs,
+    reward, done) packed in one buffer and gathered to rank 0 with ONE RCCL gather
+    on a side stream, overlapped with the next chunk (mapfx.dist.OverlappedGather).
+    Rank 0 orders a read of every chunk after its gather (stream wait, no sync)."""
     from mapfx.dist import OverlappedGather
     og = OverlappedGather(b, T, keys=("obs_window", "reward", "traj_done"), outputs=outs)
     og.step_chunk(actions=acts[:T])                  # warm the communicator
+    og.result(0)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
+    nch = K // T
     t0 = time.perf_counter()
-    for i in range(K // T):
-        og.step_chunk(actions=acts[WU + i * T:WU + (i + 1) * T])
+    for i in range(nch):
+        og.step_chunk(actions=acts[k0 + i * T:k0 + (i + 1) * T])
+        og.result(og.i - 1)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     dist.barrier()
     t = torch.tensor([el], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
-    return {"value": round(world * E * N * K / el, 1), "ms_per_step": round(el / K * 1e3, 5),
-            "bytes_per_rank_per_chunk": int(og.bytes_per_chunk()), "chunk_steps": T,
-            "collective": "torch.distributed.gather (RCCL) to rank 0 on a side stream"}
+    return {"value": round(world * E * N * nch * T / el, 1),
+            "ms_per_step": round(el / (nch * T) * 1e3, 5),
+            "steps": nch * T, "chunk_steps": T,
+            "bytes_per_rank_per_chunk": int(og.bytes_per_chunk()),
+            "collective": "one torch.distributed.gather (RCCL) per chunk to rank 0 on a side "
+                          "stream, packed (obs_window, reward, done) buffer"}
 
 
 PARTIAL_YAML = dict(  # MARL-curve-main/src/config/envs/marl_partial.yaml:3-23
@@ -348,6 +487,9 @@ def run_partial(args, dist, rank, world, local):
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)       # create the HIP events outside the timed region
+    e1.record(stream)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(stream)
     for _ in range(K // limit):

@@ -1148,6 +1148,24 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
 #endif
   constexpr int AB = ROLL ? MAPFX_AB : 1;
   uint32_t actpk[(AB + 3) / 4];
+  // Action blocks from memory are prefetched one block ahead: block 0 is issued
+  // with the state loads (its HBM latency overlaps the map build), block b + 1 as
+  // soon as block b is unpacked, so the wait at a block boundary finds it arrived.
+  int nxt[AB];
+  const bool act_mem = do_step && !a.use_rng;
+  const auto fetch = [&](int s0) {
+    if (!ROLL || a.act_dtype != MAPFX_I8) {
+#pragma unroll
+      for (int k = 0; k < AB; ++k)
+        nxt[k] = (has && s0 + k < T) ? load_action(a.actions, a.act_dtype, (uint32_t)(s0 + k) * EN + oa) : 4;
+    } else {  // int8 buffer: AB unconditional loads (clamped addresses)
+      const int8_t* ap = (const int8_t*)a.actions;
+      const uint32_t oc_ = has ? oa : 0u;
+#pragma unroll
+      for (int k = 0; k < AB; ++k) nxt[k] = ap[(uint32_t)min(s0 + k, T - 1) * EN + oc_];
+    }
+  };
+  if (act_mem) fetch(0);
 
   // ---- bitmap -> LDS, padded map, agents ----
   if (env_ok) {
@@ -1382,16 +1400,10 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
       } else if (a.use_rng) {
 #pragma unroll
         for (int k = 0; k < AB; ++k) v[k] = gen_action(a.seed, g.env_offset + env, a.t0 + s + k, ag);
-      } else if (!ROLL || a.act_dtype != MAPFX_I8) {
+      } else {  // the prefetched block; the next one is issued right away
 #pragma unroll
-        for (int k = 0; k < AB; ++k)
-          v[k] = (has && s + k < T) ? load_action(a.actions, a.act_dtype, (uint32_t)(s + k) * EN + oa)
-                                    : 4;
-      } else {  // int8 buffer: AB unconditional loads (clamped addresses), one wait
-        const int8_t* ap = (const int8_t*)a.actions;
-        const uint32_t oc_ = has ? oa : 0u;
-#pragma unroll
-        for (int k = 0; k < AB; ++k) v[k] = ap[(uint32_t)min(s + k, T - 1) * EN + oc_];
+        for (int k = 0; k < AB; ++k) v[k] = nxt[k];
+        if (ROLL && s + AB < T) fetch(s + AB);
       }
 #pragma unroll
       for (int k = 0; k < (AB + 3) / 4; ++k) actpk[k] = 0;

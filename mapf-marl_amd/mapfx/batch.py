@@ -100,6 +100,7 @@ class MapfGridBatch:
         self.obs_elem = torch.int8 if lib.mapfx_obs_elem_size(self.N) == 1 else torch.int16
         self.out = self._alloc_out(None)
         self._out_cache = {}          # outputs selection -> Out struct over self.out
+        self._traj_cache = {}         # (id(traj), outputs) -> Out struct over a trajectory
         self._dev_index = self.device.index if self.device.index is not None \
             else torch.cuda.current_device()
         self._act_shape = (self.E, self.N)
@@ -108,32 +109,37 @@ class MapfGridBatch:
                                  steps=ptr(self.steps), map_bits=ptr(self.bits))
 
     # ------------------------------------------------------------------ buffers
-    def _alloc_out(self, T):
-        E, N, dev = self.E, self.N, self.device
-        lead = () if T is None else (T,)
+    def out_spec(self, T=None):
+        """name -> (shape, dtype) of every output a step (T None) or a T-step
+        rollout (leading [T]) can write (include/mapfx.h mapfx_out)."""
+        E, N = self.E, self.N
+        lead = () if T is None else (int(T),)
         o = {
-            "reward": torch.zeros(lead + (E,), dtype=torch.float64, device=dev),
-            "reward_f32": torch.zeros(lead + (E,), dtype=torch.float32, device=dev),
-            "term": torch.zeros(lead + (E,), dtype=torch.uint8, device=dev),
-            "node": torch.zeros(lead + (E, N), dtype=torch.uint8, device=dev),
-            "edge": torch.zeros(lead + (E, N), dtype=torch.uint8, device=dev),
-            "avail": torch.zeros(lead + (E, N), dtype=torch.uint8, device=dev),
+            "reward": (lead + (E,), torch.float64),
+            "reward_f32": (lead + (E,), torch.float32),
+            "term": (lead + (E,), torch.uint8),
+            "node": (lead + (E, N), torch.uint8),
+            "edge": (lead + (E, N), torch.uint8),
+            "avail": (lead + (E, N), torch.uint8),
         }
         if "full" in self.obs_kinds:
-            o["obs_full"] = torch.zeros(lead + (E, self.H * self.W), dtype=self.obs_elem,
-                                        device=dev)
+            o["obs_full"] = (lead + (E, self.H * self.W), self.obs_elem)
         if "window" in self.obs_kinds:
             w = self.window
-            o["obs_window"] = torch.zeros(lead + (E, N, 2, w, w), dtype=self.obs_elem, device=dev)
+            o["obs_window"] = (lead + (E, N, 2, w, w), self.obs_elem)
         if "primal" in self.obs_kinds:
             s = self.primal_size
-            o["obs_primal"] = torch.zeros(lead + (E, N, 4, s, s), dtype=torch.uint8, device=dev)
-            o["primal_vec"] = torch.zeros(lead + (E, N, 3), dtype=torch.float64, device=dev)
+            o["obs_primal"] = (lead + (E, N, 4, s, s), torch.uint8)
+            o["primal_vec"] = (lead + (E, N, 3), torch.float64)
         if T is not None:
-            o["traj_pos"] = torch.zeros((T, E, N, 2), dtype=torch.int32, device=dev)
-            o["traj_done"] = torch.zeros((T, E, N), dtype=torch.uint8, device=dev)
-            o["traj_t"] = torch.zeros((T, E), dtype=torch.int32, device=dev)
+            o["traj_pos"] = ((T, E, N, 2), torch.int32)
+            o["traj_done"] = ((T, E, N), torch.uint8)
+            o["traj_t"] = ((T, E), torch.int32)
         return o
+
+    def _alloc_out(self, T):
+        return {k: torch.zeros(shape, dtype=dt, device=self.device)
+                for k, (shape, dt) in self.out_spec(T).items()}
 
     def _own_out(self, keys):
         """Cached Out struct over the persistent self.out buffers."""
@@ -209,27 +215,57 @@ class MapfGridBatch:
                          _DTYPES[a.dtype], ctypes.byref(o)), "mapfx_step")
         return self.out
 
+    def _traj_struct(self, traj, outputs):
+        """Out struct over a caller's trajectory dict, cached per (dict, outputs):
+        repeated rollouts into the same buffers build no ctypes objects."""
+        k = (id(traj), None if outputs is None else tuple(outputs))
+        hit = self._traj_cache.get(k)
+        if hit is not None and hit[0] is traj and all(
+                hit[1].get(n) is traj.get(n) for n in hit[1]):
+            return hit[2]
+        s = self._out_struct(traj, keys=k[1])
+        if len(self._traj_cache) > 64:
+            self._traj_cache.clear()
+        self._traj_cache[k] = (traj, dict(traj), s)
+        return s
+
+    def _rollout_actions(self, T, actions):
+        if actions is None:
+            return None, None, MAPFX_I8
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype not in _DTYPES:
+            a = a.to(torch.int64)
+        a = a.contiguous()
+        if tuple(a.shape) != (T, self.E, self.N):
+            raise AssertionError("actions must be [T, E, N]")
+        return a, ptr(a), _DTYPES[a.dtype]
+
     def rollout(self, T, actions=None, seed=0, t0=0, autoreset=False, traj=None, outputs=None):
         """T fused steps in one launch.  actions: [T, E, N] tensor or None (device
         generator keyed by (seed, global env, t0+k, agent)).  Returns the
         trajectory dict ([T, ...] tensors), allocated unless `traj` is given."""
         if traj is None:
             traj = self._alloc_out(T)
-        ap, adt = None, MAPFX_I8
-        if actions is not None:
-            actions = torch.as_tensor(actions, device=self.device)
-            if actions.dtype not in _DTYPES:
-                actions = actions.to(torch.int64)
-            actions = actions.contiguous()
-            if tuple(actions.shape) != (T, self.E, self.N):
-                raise AssertionError("actions must be [T, E, N]")
-            ap, adt = ptr(actions), _DTYPES[actions.dtype]
-        o = self._out_struct(traj, keys=outputs)
-        with torch.cuda.device(self.device):
-            check(lib.mapfx_rollout(self._h, ctypes.byref(self._state), int(T), ap, adt,
-                                    int(seed) & 0xFFFFFFFFFFFFFFFF, int(t0), 1 if autoreset else 0,
-                                    ctypes.byref(o), _stream_handle()), "mapfx_rollout")
+        actions, ap, adt = self._rollout_actions(T, actions)
+        o = self._traj_struct(traj, outputs)
+        check(self._call(lib.mapfx_rollout, self._h, ctypes.byref(self._state), int(T), ap, adt,
+                         int(seed) & 0xFFFFFFFFFFFFFFFF, int(t0), 1 if autoreset else 0,
+                         ctypes.byref(o)), "mapfx_rollout")
         return traj
+
+    def rollout_plan(self, T, actions=None, seed=0, t0=0, autoreset=False, traj=None,
+                     outputs=None, stream=None):
+        """A prepared `rollout` launch: every argument is converted once, so calling
+        the returned plan is one ctypes call (no tensor checks, no struct building).
+        The plan keeps `actions` / `traj` alive and launches on `stream` (default:
+        the current stream now).  Used where host time per launch matters (bench)."""
+        if traj is None:
+            traj = self._alloc_out(T)
+        actions, ap, adt = self._rollout_actions(T, actions)
+        return RolloutPlan(self, int(T), actions, ap, adt, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                           int(t0), 1 if autoreset else 0, traj,
+                           self._out_struct(traj, keys=None if outputs is None else tuple(outputs)),
+                           stream if stream is not None else torch.cuda.current_stream(self.device))
 
     def gen_actions(self, T, seed, t0=0, out=None):
         if out is None:
@@ -258,3 +294,25 @@ class MapfGridBatch:
         """[E, N, H*W] view: every agent observes the same occupancy map (:161-183)."""
         o = self.out["obs_full"]
         return o.unsqueeze(1).expand(self.E, self.N, o.shape[-1])
+
+
+class RolloutPlan:
+    """One prepared `mapfx_rollout` launch (MapfGridBatch.rollout_plan).
+
+    Holds the ctypes arguments ready-made: __call__ is a single foreign call on
+    the plan's stream.  `traj` is the trajectory dict the launch writes."""
+
+    __slots__ = ("batch", "T", "actions", "traj", "_fn", "_args")
+
+    def __init__(self, batch, T, actions, ap, adt, seed, t0, autoreset, traj, out, stream):
+        self.batch, self.T, self.actions, self.traj = batch, T, actions, traj
+        self._fn = lib.mapfx_rollout
+        # byref objects keep `out` and the state struct alive with the plan
+        self._args = (batch._h, ctypes.byref(batch._state), T, ap, adt, seed, t0, autoreset,
+                      ctypes.byref(out), stream.cuda_stream)
+
+    def __call__(self):
+        rc = self._fn(*self._args)
+        if rc:
+            check(rc, "mapfx_rollout")
+        return self.traj

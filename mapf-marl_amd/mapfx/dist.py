@@ -7,9 +7,11 @@ is bit-identical, env for env, to a single-GPU run of all envs.
 
 The only collective is the one the reference's runner architecture implies:
 ParallelRunner collects every worker env's (obs, reward, done) in the parent
-process (runners/parallel_runner.py:117-173).  Here that is a torch.distributed
-gather (RCCL over xGMI with the "nccl" backend) of a rollout chunk's trajectory
-tensors to rank 0, issued on a side stream so it overlaps the next chunk.
+process (runners/parallel_runner.py:117-173).  Here that is ONE torch.distributed
+gather (RCCL over xGMI with the "nccl" backend) per rollout chunk: the chunk's
+trajectory tensors live in one flat byte buffer (ChunkLayout) whose gathered
+keys form a contiguous prefix, issued on a side stream so it overlaps the next
+chunk.  Both the send buffers and rank 0's receive buffers are double-buffered.
 """
 from __future__ import annotations
 
@@ -56,49 +58,155 @@ def concat_env_major(parts, env_dim: int):
     return torch.cat(parts, dim=env_dim)
 
 
-class OverlappedGather:
-    """Double-buffered trajectory chunks: chunk i is gathered to rank 0 on a side
-    stream while chunk i+1 is being stepped on the compute stream."""
+def _nbytes(shape, dtype):
+    n = torch.empty((), dtype=dtype).element_size()
+    for s in shape:
+        n *= int(s)
+    return n
 
-    def __init__(self, batch, T: int, keys=("obs_window", "reward", "traj_done"), outputs=None):
+
+class ChunkLayout:
+    """Several typed tensors carved out of ONE flat uint8 buffer.
+
+    `spec` maps name -> (shape, dtype); names are laid out in `order` (the
+    rest of `spec` after it), each at a 16-byte aligned offset, so the first k
+    names form a contiguous prefix that one collective can move."""
+
+    ALIGN = 16
+
+    def __init__(self, spec: dict, order=()):
+        names = [k for k in order if k in spec] + [k for k in spec if k not in order]
+        missing = [k for k in order if k not in spec]
+        if missing:
+            raise KeyError("ChunkLayout: %s not in the output spec" % missing)
+        self.spec = {k: (tuple(int(s) for s in spec[k][0]), spec[k][1]) for k in names}
+        self.offsets = {}
+        off = 0
+        for k in names:
+            self.offsets[k] = off
+            off += -(-_nbytes(*self.spec[k]) // self.ALIGN) * self.ALIGN
+        self.nbytes = off
+
+    def end_of(self, keys):
+        """Bytes of the prefix holding `keys` (which must be a prefix of the order)."""
+        names = list(self.spec)
+        if list(keys) != names[:len(keys)]:
+            raise ValueError("keys %s are not a prefix of the layout %s" % (list(keys), names))
+        if not keys:
+            return 0
+        k = keys[-1]
+        return self.offsets[k] + _nbytes(*self.spec[k])
+
+    def alloc(self, device):
+        return torch.zeros(self.nbytes, dtype=torch.uint8, device=device)
+
+    def views(self, flat, keys=None):
+        """name -> typed view into `flat` ([nbytes] or [R, >=nbytes] uint8: then
+        each view gets a leading R dimension)."""
+        out = {}
+        for k in (self.spec if keys is None else keys):
+            shape, dt = self.spec[k]
+            o, n = self.offsets[k], _nbytes(shape, dt)
+            v = flat[..., o:o + n].view(dt)
+            out[k] = v.unflatten(-1, shape) if shape else v.view(flat.shape[:-1])
+        return out
+
+
+class OverlappedGather:
+    """Rollout chunks with ONE gather of each chunk's (obs, reward, done) to `dst`.
+
+    Chunk i is stepped on the current stream into send buffer i % 2 and gathered
+    on a side stream into receive buffer i % 2 while chunk i+1 steps.  Ordering:
+      * the rollout into send buffer s waits for the previous gather out of s;
+      * the gather into receive buffer s waits for everything enqueued on the
+        current stream before step_chunk() was called, so a consumer's reads of
+        chunk i (kernels on the current stream, or host copies) that come before
+        step_chunk(i + 2) never race the overwrite;
+      * result(i) makes the current stream wait for chunk i's gather (no host sync).
+    On a CPU device (gloo) everything is synchronous on the calling thread.
+    """
+
+    def __init__(self, batch, T: int, keys=("obs_window", "reward", "traj_done"), outputs=None,
+                 dst: int = 0, group=None):
         import torch.distributed as dist
         self.dist = dist
         self.batch = batch
-        self.T = T
+        self.T = int(T)
         self.keys = tuple(keys)
         self.outputs = outputs
-        self.bufs = [batch._alloc_out(T), batch._alloc_out(T)]
-        self.side = torch.cuda.Stream(device=batch.device)
-        self.done_ev = [None, None]
-        self.rank = dist.get_rank()
-        self.world = dist.get_world_size()
+        self.dst, self.group = dst, group
+        self.layout = ChunkLayout(batch.out_spec(self.T), order=self.keys)
+        # whole 16-B units, so every typed view of a received row stays aligned
+        self.gbytes = -(-self.layout.end_of(self.keys) // ChunkLayout.ALIGN) * ChunkLayout.ALIGN
+        dev = batch.device
+        self.cuda = torch.device(dev).type == "cuda"
+        self.flat = [self.layout.alloc(dev), self.layout.alloc(dev)]
+        self.bufs = [self.layout.views(f) for f in self.flat]
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
         self.recv = None
-        if self.rank == 0:
-            self.recv = {k: [torch.empty_like(self.bufs[0][k]) for _ in range(self.world)]
-                         for k in self.keys}
+        if self.rank == dst:
+            self.recv = [torch.empty((self.world, self.gbytes), dtype=torch.uint8, device=dev)
+                         for _ in range(2)]
+        self.side = torch.cuda.Stream(device=dev) if self.cuda else None
+        self.gather_ev = [None, None]
         self.i = 0
 
     def bytes_per_chunk(self):
-        return sum(self.bufs[0][k].numel() * self.bufs[0][k].element_size() for k in self.keys)
+        """Bytes one rank sends per chunk (the gathered prefix)."""
+        return self.gbytes
+
+    def _gather(self, cur):
+        lst = list(self.recv[cur].unbind(0)) if self.rank == self.dst else None
+        self.dist.gather(self.flat[cur][:self.gbytes], gather_list=lst, dst=self.dst,
+                         group=self.group)
 
     def step_chunk(self, actions=None, seed=0, t0=0):
-        cur = self.i & 1
-        if self.done_ev[cur] is not None:  # buffer reuse: its gather must be finished
-            torch.cuda.current_stream().wait_event(self.done_ev[cur])
-        traj = self.batch.rollout(self.T, actions=actions, seed=seed, t0=t0, traj=self.bufs[cur],
-                                  outputs=self.outputs)
+        """Step one chunk and start its gather.  Returns the chunk index."""
+        i, cur = self.i, self.i & 1
+        if not self.cuda:
+            self.batch.rollout(self.T, actions=actions, seed=seed, t0=t0, traj=self.bufs[cur],
+                               outputs=self.outputs)
+            self._gather(cur)
+            self.i += 1
+            return i
+        cs = torch.cuda.current_stream(self.batch.device)
+        if self.gather_ev[cur] is not None:      # send buffer reuse: its gather must be done
+            cs.wait_event(self.gather_ev[cur])
+        self.batch.rollout(self.T, actions=actions, seed=seed, t0=t0, traj=self.bufs[cur],
+                           outputs=self.outputs)
         ready = torch.cuda.Event()
-        ready.record()
+        ready.record(cs)
         with torch.cuda.stream(self.side):
             self.side.wait_event(ready)
-            for k in self.keys:
-                self.dist.gather(traj[k], gather_list=self.recv[k] if self.rank == 0 else None,
-                                 dst=0)
+            self._gather(cur)
             ev = torch.cuda.Event()
             ev.record(self.side)
-            self.done_ev[cur] = ev
+            self.gather_ev[cur] = ev
         self.i += 1
-        return traj
+        return i
+
+    def local(self, i):
+        """This rank's trajectory tensors of chunk i (valid until step_chunk(i + 2))."""
+        self._check(i)
+        return self.bufs[i & 1]
+
+    def result(self, i):
+        """On dst: chunk i's gathered tensors, key -> [world, T, E_rank, ...] (rank
+        order = global env order).  Valid until step_chunk(i + 2) is called."""
+        self._check(i)
+        if self.rank != self.dst:
+            return None
+        cur = i & 1
+        if self.cuda and self.gather_ev[cur] is not None:
+            torch.cuda.current_stream(self.batch.device).wait_event(self.gather_ev[cur])
+        return self.layout.views(self.recv[cur], self.keys)
+
+    def _check(self, i):
+        if not self.i - 2 <= i < self.i:
+            raise IndexError("chunk %d is not resident (chunks %d..%d are)"
+                             % (i, max(0, self.i - 2), self.i - 1))
 
     def synchronize(self):
-        torch.cuda.synchronize(self.batch.device)
+        if self.cuda:
+            torch.cuda.synchronize(self.batch.device)

@@ -13,6 +13,8 @@
 """
 from __future__ import annotations
 
+import io
+
 import numpy as np
 
 from . import rng
@@ -26,13 +28,22 @@ def map_stride(h: int, w: int) -> int:
 
 
 def parse_map_text(text: str) -> np.ndarray:
-    """envs/mapf_gridworld.py:421-428 + :282-288 -> int8 grid (-1 obstacle, 0 free)."""
-    rows = [row.rstrip() for row in text.splitlines()][4:]
+    """envs/mapf_gridworld.py:421-428 + :282-288 -> int8 grid (-1 obstacle, 0 free).
+
+    Lines are split exactly as the reference's text-mode `f.readlines()` splits
+    them (universal newlines: \\n, \\r\\n, \\r -- not \\v, \\f or \\u2028), then
+    rstrip()ed; 4 header lines.  A row shorter than row 0 raises IndexError, as
+    the reference's `_original_grid[i][j]` does; longer rows are cut at row 0's
+    width (the reference never reads past it)."""
+    rows = [row.rstrip() for row in io.StringIO(text, newline=None).readlines()][4:]
     if not rows or not rows[0]:
         raise AssertionError("empty map")
     w = len(rows[0])
     arr = np.full((len(rows), w), -1, dtype=np.int8)
     for i, row in enumerate(rows):
+        if len(row) < w:
+            raise IndexError("string index out of range (map row %d has %d of %d cells)"
+                             % (i, len(row), w))
         for j, ch in enumerate(row[:w]):
             if ch == ".":
                 arr[i, j] = 0

@@ -99,3 +99,163 @@ def test_shard_bounds():
                 assert o1 + c1 == o2
             assert sum(c for _, c in spans) == n
             assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+
+
+# ---------------------------------------------------------------- launcher + packed gather
+def _run_bench(*argv, timeout=180):
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + list(argv),
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                          timeout=timeout, env=env)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launcher_spawns_ranks(world):
+    """bench.py --gpus N with no torchrun environment starts N ranks itself
+    (launch_ranks): the gloo rehearsal of the same path shards global env ids and
+    gathers one packed buffer per rank to rank 0."""
+    import json
+    r = _run_bench("--gpus", str(world), "--dist-selftest")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout           # rank 0 prints, the others stay quiet
+    assert lines[0]["dist_selftest"] == "ok"
+    assert lines[0]["n_gpus"] == world and lines[0]["launcher"] == "bench.py launch_ranks"
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    n = max(2, torch.cuda.device_count() + 1)
+    r = _run_bench("--gpus", str(n), "--steps", "2", "--warmup", "0")
+    assert r.returncode != 0
+    assert "requested but only" in r.stderr
+    assert not any(x.startswith("{") for x in r.stdout.splitlines())
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                        "--dist-selftest"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_chunk_layout_prefix_and_views():
+    from mapfx.dist import ChunkLayout
+    spec = {"a": ((3, 5), torch.float64), "b": ((7,), torch.uint8), "c": ((2, 3), torch.int32),
+            "d": ((), torch.int64)}
+    lay = ChunkLayout(spec, order=("b", "a"))
+    assert list(lay.spec) == ["b", "a", "c", "d"]
+    assert all(o % 16 == 0 for o in lay.offsets.values())
+    assert lay.end_of(("b",)) == 7 and lay.end_of(("b", "a")) == 16 + 120
+    with pytest.raises(ValueError):
+        lay.end_of(("a",))
+    flat = lay.alloc("cpu")
+    v = lay.views(flat)
+    v["a"].copy_(torch.arange(15, dtype=torch.float64).view(3, 5))
+    v["b"].fill_(9)
+    v["c"].copy_(torch.tensor([[1, 2, 3], [4, 5, 6]], dtype=torch.int32))
+    v["d"].fill_(-5)
+    two = torch.stack([flat, flat.clone()])
+    v2 = lay.views(two)
+    assert v2["a"].shape == (2, 3, 5) and torch.equal(v2["a"][1], v["a"])
+    assert torch.equal(v2["c"][0], v["c"]) and v2["d"].tolist() == [-5, -5]
+    with pytest.raises(KeyError):
+        ChunkLayout(spec, order=("zz",))
+
+
+class _OracleTrajBatch:
+    """Test stand-in for MapfGridBatch on a CPU rank: the C oracle steps the
+    shard, and rollout() fills [T, ...] trajectory tensors like mapfx_rollout."""
+
+    def __init__(self, inst, S, N, W, offset):
+        from oracle import corc
+        self.corc = corc
+        self.E, self.N, self.W, self.offset = inst["init_pos"].shape[0], N, W, offset
+        self.device = torch.device("cpu")
+        self.ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=7,
+                                   env_offset=offset, nthreads=1)
+
+    def out_spec(self, T):
+        E, N, W = self.E, self.N, self.W
+        return {"obs_window": ((T, E, N, 2, W, W), torch.int8), "reward": ((T, E), torch.float64),
+                "traj_done": ((T, E, N), torch.uint8), "traj_pos": ((T, E, N, 2), torch.int32)}
+
+    def rollout(self, T, actions=None, seed=0, t0=0, traj=None, outputs=None):
+        lib = self.corc.lib()
+        for k in range(T):
+            a = np.array([[lib.orc_action(seed, self.offset + e, t0 + k, i) for i in range(self.N)]
+                          for e in range(self.E)], dtype=np.int32)
+            r = self.ob.step(a)
+            o = self.ob.observe(window=self.W, full=False)
+            traj["reward"][k].copy_(torch.from_numpy(r["reward"]))
+            traj["obs_window"][k].copy_(torch.from_numpy(o["obs_window"]))
+            traj["traj_done"][k].copy_(torch.from_numpy(self.ob.done))
+            traj["traj_pos"][k].copy_(torch.from_numpy(self.ob.pos))
+        return traj
+
+
+_OG = dict(S=12, N=6, W=5, T=3, chunks=3, E=5)
+
+
+def _og_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [REPO, PKG_ROOT]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mapfx.dist import OverlappedGather
+        from mapfx.maps import synthetic_instances
+        c = _OG
+        inst = synthetic_instances(c["E"], c["S"], c["S"], c["N"], p_obstacle=0.1, seed=5,
+                                   env_offset=rank * c["E"])
+        fb = _OracleTrajBatch(inst, c["S"], c["N"], c["W"], rank * c["E"])
+        og = OverlappedGather(fb, c["T"])
+        assert og.bytes_per_chunk() % 16 == 0
+        got = []
+        for i in range(c["chunks"]):
+            og.step_chunk(seed=9, t0=i * c["T"])
+            res = og.result(i)
+            if rank == 0:
+                got.append({k: v.clone().numpy() for k, v in res.items()})
+            with pytest.raises(IndexError):
+                og.result(i - 2) if i >= 2 else og.result(i + 1)
+        if rank == 0:
+            q.put(got)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_gather_packed_world2():
+    """OverlappedGather at world 2 (gloo): ONE gather per chunk of the packed
+    (obs_window, reward, done) prefix, double-buffered receive side; rank 0's
+    per-chunk result equals an unsharded run, env for env."""
+    from mapfx.maps import synthetic_instances
+    world, c = 2, _OG
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_og_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    inst = synthetic_instances(world * c["E"], c["S"], c["S"], c["N"], p_obstacle=0.1, seed=5)
+    fb = _OracleTrajBatch(inst, c["S"], c["N"], c["W"], 0)
+    for i in range(c["chunks"]):
+        traj = {k: torch.zeros(s, dtype=d) for k, (s, d) in fb.out_spec(c["T"]).items()}
+        fb.rollout(c["T"], seed=9, t0=i * c["T"], traj=traj)
+        g = got[i]
+        assert set(g) == {"obs_window", "reward", "traj_done"}
+        for k in g:
+            # [world, T, E_rank, ...] -> [T, world * E_rank, ...]
+            merged = np.concatenate(list(g[k]), axis=1)
+            assert np.array_equal(merged.view(np.uint8), traj[k].numpy().view(np.uint8)), (i, k)

@@ -440,8 +440,11 @@ def test_sharded_batches_equal_full_batch(mapfx_mod):
 
 
 def test_overlapped_gather_single_rank(mapfx_mod):
-    """OverlappedGather on a 1-rank RCCL group: rank 0's received chunk equals the
-    chunk it stepped, for both double buffers."""
+    """OverlappedGather on a 1-rank RCCL group, read the way a consumer does: each
+    chunk's gathered tensors are cloned on the current stream right after
+    step_chunk (result() orders the read after the gather with a stream wait, no
+    device sync), for 5 chunks through both receive buffers.  Every clone must
+    equal a plain rollout of the same chunk."""
     import os
     import socket
     import torch.distributed as dist
@@ -456,14 +459,22 @@ def test_overlapped_gather_single_rank(mapfx_mod):
     try:
         E, S, N, T = 256, 32, 16, 8
         inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=2)
-        b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"],
-                                    hw=(S, S), episode_limit=100, obs=("window",))
+        mk = lambda: mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"],
+                                             hw=(S, S), episode_limit=100, obs=("window",))
+        b, bref = mk(), mk()
         b.reset()
+        bref.reset()
         og = OverlappedGather(b, T)
-        for i in range(3):
-            tr = og.step_chunk(seed=4, t0=i * T)
-            og.synchronize()
+        got = []
+        for i in range(5):
+            og.step_chunk(seed=4, t0=i * T)
+            got.append({k: v[0].clone() for k, v in og.result(i).items()})
+        ref = [{k: v.clone() for k, v in bref.rollout(T, seed=4, t0=i * T).items()}
+               for i in range(5)]
+        torch.cuda.synchronize()
+        assert og.bytes_per_chunk() % 16 == 0
+        for i in range(5):
             for k in og.keys:
-                assert torch.equal(og.recv[k][0], tr[k]), (i, k)
+                assert torch.equal(got[i][k], ref[i][k]), (i, k)
     finally:
         dist.destroy_process_group()

@@ -100,7 +100,11 @@ struct Geo {
   int wv_off_map, wv_off_dep, wv_off_bits, wv_off_rew, wv_off_stage, wv_lds;
   int wv_bits_env_bytes, wv_rew_buf, wv_stage_buf, wv_rew_row;  // rew / staging are double-buffered
   int wv_off_split, wv_split_buf;  // store-wave split: double-buffered per-step output image
+  int wv_fast;                     // build_map_rows_fast applies (W <= 64, pitch % 8 == 0)
 };
+#ifndef MAPFX_FAST_WPR
+#define MAPFX_FAST_WPR 24  // words per padded row handled by build_map_rows_fast
+#endif
 
 struct Args {
   int32_t* pos;
@@ -613,42 +617,55 @@ __device__ unsigned long long g_stamps[256 * 8];
     __builtin_amdgcn_sched_barrier(0);                                            \
     if (blockIdx.x == 0 && threadIdx.x == 0 && s < 256) g_stamps[s * 8 + (k)] = t_; \
   } while (0)
+// prologue / epilogue stamps of block 0 / lane 0 (row 255 of g_stamps)
+#define PSTAMP(k)                                                                 \
+  do {                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    unsigned long long t_;                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[255 * 8 + (k)] = t_;       \
+  } while (0)
 #else
 #define STAMP(k) \
   do {           \
   } while (0)
+#define PSTAMP(k) \
+  do {            \
+  } while (0)
 #endif
 
-// Wave-path cell format: one byte per padded cell, c = count + 1 - obstacle, so
+// Wave-path cell format: one byte per padded cell = (obstacle << 7) | c with
+// c = count + 1 - obstacle (7 bits), so
 //   c == 0  <=> obstacle with no agent on it (and every border cell): the move /
 //               avail / window "obstacle" test of the reference (:278-280, :209-222,
-//               marl_partial.py:335-337) is a plain zero test;
+//               marl_partial.py:335-337) is a zero test of the low 7 bits;
 //   agents plane = max(count - obstacle, 0) = c - (c != 0);  occ = c - 1;
-// and adding / removing an agent is +-1 with no borrow (c >= 1 under an agent).
-// The static obstacle flag lives in bit 7 of the per-cell `dep` byte (the low 7
-// bits hold the move direction of the cell's occupant in the current step).
-// Built one map row per lane at a time: border rows / pad words are constant, an
-// interior word is one 4-bit window of the bitmap row spread over four cells.
-__device__ inline void build_map_rows_c(const Geo& g, uint32_t* map32, uint32_t* dep32,
-                                        const uint32_t* bitsL, int lane, int nl) {
+//   count = c - 1 + obstacle (bit 7: the static obstacle flag rides with the cell);
+// and adding / removing an agent is +-1 with no borrow out of the 7 bits (c >= 1
+// under an agent).  The per-cell `dep` byte (move direction of the cell's occupant
+// in the current step) is written by every occupant before it is read and needs no
+// initialisation.
+// Fallback builder (rows wider than build_map_rows_fast handles): one map row per
+// lane at a time, border rows / pad words constant, an interior word one 4-bit
+// window of the bitmap row (staged in LDS) spread over four cells.
+__device__ __forceinline__ uint32_t cells_of_nibble(uint32_t nib) {  // 4 obstacle bits -> 4 cells
+  const uint32_t f = (nib * 0x00204081u) & 0x01010101u;
+  return (f << 7) | (f ^ 0x01010101u);
+}
+__device__ inline void build_map_rows_c(const Geo& g, uint32_t* map32, const uint32_t* bitsL, int lane,
+                                        int nl) {
   const int wpr = g.wpr, plw = g.pl >> 2;
   const int iw = (g.W + 3) >> 2;  // interior words (the last one may hold border cells)
   const uint32_t last_or = (g.W & 3) ? ((0xFu << (g.W & 3)) & 0xFu) : 0u;
   for (int pr = lane; pr < g.rows; pr += nl) {
     uint32_t* row = map32 + pr * wpr;
-    uint32_t* drow = dep32 + pr * wpr;
     const int rr = pr - g.P;
     if (rr < 0 || rr >= g.H) {
-      for (int w = 0; w < wpr; ++w) {
-        row[w] = 0u;
-        drow[w] = 0xFFFFFFFFu;
-      }
+      for (int w = 0; w < wpr; ++w) row[w] = 0x80808080u;
       continue;
     }
-    for (int w = 0; w < plw; ++w) {
-      row[w] = 0u;
-      drow[w] = 0xFFFFFFFFu;
-    }
+    for (int w = 0; w < plw; ++w) row[w] = 0x80808080u;
     // 32 cells (8 map words) per bitmap read pair: the reads of a chunk are waited
     // for once, not once per word
     for (int k0 = 0; k0 < iw; k0 += 8) {
@@ -659,16 +676,70 @@ __device__ inline void build_map_rows_c(const Geo& g, uint32_t* map32, uint32_t*
         if (k0 + j < iw) {
           uint32_t nib = (x >> (4 * j)) & 0xFu;
           if (k0 + j == iw - 1) nib |= last_or;
-          const uint32_t f = (nib * 0x00204081u) & 0x01010101u;  // obstacle flag per cell
-          row[plw + k0 + j] = f ^ 0x01010101u;
-          drow[plw + k0 + j] = (f << 7) | 0x7F7F7F7Fu;
+          row[plw + k0 + j] = cells_of_nibble(nib);
         }
       }
     }
-    for (int w = plw + iw; w < wpr; ++w) {
-      row[w] = 0u;
-      drow[w] = 0xFFFFFFFFu;
+    for (int w = plw + iw; w < wpr; ++w) row[w] = 0x80808080u;
+  }
+}
+
+// Fast builder for padded rows of at most MAXW words (W <= 64, pitch % 8 == 0):
+// each lane builds whole rows, branch-free, from the env's bitmap words read
+// straight from global memory (L2 hits after the env's first lane -- no LDS
+// staging, no fence), two cell words per ds_write_b64.  The padded row's
+// obstacle bits (1 = obstacle, the border included) sit in lo (cells 0-63) / hi.
+// The bitmap words of a lane's first RPF rows are loaded by fast_row_prefetch at
+// kernel entry, so their latency overlaps the state loads.
+template <int RPF>
+__device__ __forceinline__ void fast_row_prefetch(const Geo& g, const uint32_t* src, int lane, int nl,
+                                                  uint32_t (&pf)[RPF][3]) {
+  const int last = g.bits_words - 1;
+#pragma unroll
+  for (int k = 0; k < RPF; ++k) {
+    const int rr = min(max(lane + k * nl - g.P, 0), g.H - 1);  // clamped: always a valid address
+    const int i0 = (rr * g.W) >> 5;
+    pf[k][0] = src[i0];
+    pf[k][1] = src[min(i0 + 1, last)];
+    pf[k][2] = src[min(i0 + 2, last)];
+  }
+}
+template <int MAXW, int RPF>
+__device__ inline void build_map_rows_fast(const Geo& g, uint32_t* map32, const uint32_t* src, int lane,
+                                           int nl, const uint32_t (&pf)[RPF][3]) {
+  const int wpr = g.wpr, pl = g.pl, e = g.pl + g.W, last = g.bits_words - 1;
+  const uint64_t wmask = g.W < 64 ? (1ull << g.W) - 1ull : ~0ull;
+  // one padded row from its bitmap words w0..w2 (the words covering bits rr*W ..)
+  const auto row = [&](int pr, uint32_t w0, uint32_t w1, uint32_t w2) {
+    const int rr = pr - g.P;
+    uint64_t lo = ~0ull;
+    uint32_t hi = ~0u;
+    if (rr >= 0 && rr < g.H) {
+      const int sh = (rr * g.W) & 31;
+      const uint64_t rb = ((((uint64_t)__builtin_amdgcn_alignbit(w2, w1, sh)) << 32) |
+                           __builtin_amdgcn_alignbit(w1, w0, sh)) & wmask;
+      lo = (rb << pl) | ((1ull << pl) - 1ull) | (e < 64 ? ~0ull << e : 0ull);  // 1 <= pl <= 32
+      hi = (uint32_t)(rb >> (64 - pl)) | (e <= 64 ? ~0u : (e < 96 ? ~0u << (e - 64) : 0u));
     }
+    uint2* row2 = (uint2*)(map32 + pr * wpr);
+#pragma unroll
+    for (int j = 0; j < MAXW / 2; ++j) {
+      if (2 * j < wpr) {
+        const int w = 2 * j;  // cells 4w .. 4w+7 of the padded row
+        const uint32_t n0 = w < 16 ? (uint32_t)(lo >> (4 * w)) : hi >> (4 * w - 64);
+        const uint32_t n1 = w + 1 < 16 ? (uint32_t)(lo >> (4 * w + 4)) : hi >> (4 * w - 60);
+        row2[j] = make_uint2(cells_of_nibble(n0 & 0xFu), cells_of_nibble(n1 & 0xFu));
+      }
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < RPF; ++k) {
+    const int pr = lane + k * nl;
+    if (pr < g.rows) row(pr, pf[k][0], pf[k][1], pf[k][2]);
+  }
+  for (int pr = lane + RPF * nl; pr < g.rows; pr += nl) {
+    const int i0 = (min(max(pr - g.P, 0), g.H - 1) * g.W) >> 5;
+    row(pr, src[i0], src[min(i0 + 1, last)], src[min(i0 + 2, last)]);
   }
 }
 
@@ -694,9 +765,10 @@ __device__ inline void wave_fence() {
 // 4 cells of the c format (one u32) -> obstacle plane bytes (c == 0) and agents
 // plane bytes (c - (c != 0)); c <= 127 so the +0x7F carry never leaves its byte.
 __device__ inline void swar_window(uint32_t v, uint32_t& ob, uint32_t& ag) {
-  const uint32_t nz = ((v + 0x7F7F7F7Fu) >> 7) & 0x01010101u;  // 1 where c >= 1
+  const uint32_t c = v & 0x7F7F7F7Fu;                            // drop the obstacle flags
+  const uint32_t nz = ((c + 0x7F7F7F7Fu) >> 7) & 0x01010101u;  // 1 where c >= 1
   ob = nz ^ 0x01010101u;
-  ag = v - nz;
+  ag = c - nz;
 }
 
 // OR a chunk of `bits` (<= 56) bits into a little-endian u64 bit stream at `pos`
@@ -915,8 +987,7 @@ struct SplitLayout {
 #define SLOT_CHUNK (MAPFX_SPLIT_SOA ? 64 : 1)
 
 // info.z flag bits
-constexpr uint32_t SF_DONE = 1, SF_LIVE = 2, SF_DNOLD = 4, SF_ENVC = 8, SF_SKIP = 16, SF_OBST = 32,
-                   SF_ALLDONE = 64;
+constexpr uint32_t SF_DONE = 1, SF_LIVE = 2, SF_DNOLD = 4, SF_ENVC = 8, SF_SKIP = 16, SF_ALLDONE = 64;
 
 // Workgroup barrier that waits for this wave's LDS traffic only: outstanding
 // global stores stay in flight (a __syncthreads() would drain them every step).
@@ -1013,10 +1084,10 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
     if constexpr (SMALL) {
       // node collision (:344-362): post-step count = c - 1 + obstacle >= 2 (centre cell)
       const uint32_t ctr = (__builtin_amdgcn_alignbyte(qx[WIN + H2], qx[H2], o) >> (8 * H2)) & 0xFFu;
-      uint32_t node = ctr + ((fl / SF_OBST) & 1u) >= 3u ? 1u : 0u;
+      uint32_t node = (ctr & 0x7Fu) + (ctr >> 7) >= 3u ? 1u : 0u;
       if (fl & SF_SKIP) node = 0;
       // avail (:203-224): a neighbour is available iff its c != 0; stay always
-      const uint32_t nzn = ((nb + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
+      const uint32_t nzn = (((nb & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
       const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
       const uint32_t edge = fl >> 8;
       // reward (:94-130, exact fp64 op order)
@@ -1098,6 +1169,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
 #ifdef MAPFX_CLOCKS
   const unsigned long long rtk0 = __builtin_amdgcn_s_memrealtime();
 #endif
+  PSTAMP(6);
   const int L = LL > 0 ? LL : g.L;
   const int lshift = LL > 0 ? (LL == 64 ? 6 : LL == 32 ? 5 : LL == 16 ? 4 : LL == 8 ? 3 : LL == 4 ? 2 : LL == 2 ? 1 : 0)
                             : g.lshift;
@@ -1129,6 +1201,11 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
 
   const uint32_t oa = (uint32_t)(env * N + ag);  // agent index inside one step slot
   const uint32_t EN = (uint32_t)(g.E * N);
+  // bitmap words of this lane's first map rows (fast build): issued first
+  const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared || !env_ok ? 0 : (long long)env * g.map_stride));
+  constexpr int RPF = 4;
+  uint32_t pfw[RPF][3];
+  if (g.wv_fast) fast_row_prefetch<RPF>(g, bsrc, ag, L, pfw);
   int cur = 0, gcell = -1, st = 0;  // padded cell of the agent / of its goal
   bool dn = false;
   if (has) {
@@ -1140,6 +1217,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
     if (a.steps) st = a.steps[oa];
   }
   int tcur = env_ok ? a.t[env] : 0;
+  PSTAMP(0);
   const int T = ROLL ? a.T : 1;
   // Actions are fetched for AB steps at a time: one VMEM wait per block instead of
   // one per step (a wait on a per-step load would also drain the step's stores).
@@ -1167,21 +1245,21 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   };
   if (act_mem) fetch(0);
 
-  // ---- bitmap -> LDS, padded map, agents ----
-  if (env_ok) {
-    const uint32_t* src =
-        (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)env * g.map_stride));
-    for (int w = ag; w < g.bits_words; w += L) bitsL[w] = src[w];
+  // ---- padded map (from the bitmap: global -> registers, or staged in LDS), agents ----
+  if (env_ok && !g.wv_fast) {
+    for (int w = ag; w < g.bits_words; w += L) bitsL[w] = bsrc[w];
   }
   if (ROLL) {  // both reward rows start at +0.0 (folds of steps < 0 read them)
     for (int i = lane64; i < 2 * rew_buf; i += 64) rewL[i] = 0.0;
   }
+  if (!g.wv_fast) wave_fence();
+  PSTAMP(1);
+  if (g.wv_fast) build_map_rows_fast<MAPFX_FAST_WPR, RPF>(g, map32, bsrc, ag, L, pfw);
+  else build_map_rows_c(g, map32, bitsL, ag, L);
   wave_fence();
-  build_map_rows_c(g, map32, (uint32_t*)dep, bitsL, ag, L);
-  wave_fence();
+  PSTAMP(2);
   if (has) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
   wave_fence();
-  uint32_t f_cur = has ? (uint32_t)dep[cur] >> 7 : 0u;  // obstacle flag of the agent's cell
 
   const auto cell_rc = [&](int cell) {  // padded cell -> (row, col); cell < 2^16, pitch < 256
     const uint32_t pr = (uint32_t)(((uint64_t)(((uint32_t)cell << 8) & 0xFFFFFFu) *
@@ -1288,7 +1366,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
       u32x4* sl = (u32x4*)__builtin_assume_aligned(
           lds + g.wv_off_split + ((qs + 1) & 1) * g.wv_split_buf + lane64 * SLOT_LANE, 16);
       const uint32_t fl = (q_dn ? SF_DONE : 0u) | (q_live ? SF_LIVE : 0u) | (q_dnold ? SF_DNOLD : 0u) |
-                          (q_envc ? SF_ENVC : 0u) | (q_skip ? SF_SKIP : 0u) | ((q_dj >> 7) ? SF_OBST : 0u) |
+                          (q_envc ? SF_ENVC : 0u) | (q_skip ? SF_SKIP : 0u) |
                           (q_alldone ? SF_ALLDONE : 0u) | ((uint32_t)(edge > 255 ? 255 : edge) << 8);
       uint32_t w[SL::SLOT / 4];
       w[0] = (uint32_t)q_nc;
@@ -1313,13 +1391,13 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
       window_regs<WIN>(qx, o, R);
       // centre cell (H2 <= 3: it lies in cells 0-3 of the middle row)
       const uint32_t ctr = (__builtin_amdgcn_alignbyte(qx[WIN + H2], qx[H2], o) >> (8 * H2)) & 0xFFu;
-      node = ctr + (q_dj >> 7) >= 3u ? 1u : 0u;            // count = c - 1 + obstacle >= 2
+      node = (ctr & 0x7Fu) + (ctr >> 7) >= 3u ? 1u : 0u;   // count = c - 1 + obstacle >= 2
     } else {
-      node = (qx[0] & 0xFFu) + (q_dj >> 7) >= 3u ? 1u : 0u;
+      node = (qx[0] & 0x7Fu) + ((qx[0] >> 7) & 1u) >= 3u ? 1u : 0u;
     }
     if (q_skip) node = 0;
     // avail (:203-224): a neighbour is available iff its c != 0; stay always
-    const uint32_t nzn = ((q_nb + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
+    const uint32_t nzn = (((q_nb & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
     const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
     if constexpr (WIN > 0) {
       if (want_win && has && !(MAPFX_ABLATE & 1)) {
@@ -1387,6 +1465,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   if (has)
     nb = (uint32_t)map[cur - pitch] | ((uint32_t)map[cur + pitch] << 8) |
          ((uint32_t)map[cur - 1] << 16) | ((uint32_t)map[cur + 1] << 24);
+  PSTAMP(3);
 #ifdef MAPFX_CLOCKS
   const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
@@ -1424,14 +1503,14 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
     // ---------------- A: move decision on the PRE-step map (:319-342) ----------------
     const int oc = cur;
     const bool mv = !dn && (uint32_t)act < 4u;  // 4 = stay, 0xFF = invalid (!has: 4)
-    const uint32_t v = mv ? ((nb >> ((act & 3) * 8)) & 0xFFu) : 0u;  // pre-step cell (c)
-    const bool envc = mv && v == 0u;  // out of bounds / free-standing obstacle (quirk 1)
+    const uint32_t v = mv ? ((nb >> ((act & 3) * 8)) & 0xFFu) : 0u;  // pre-step cell (flag | c)
+    const bool envc = mv && (v & 0x7Fu) == 0u;  // out of bounds / free-standing obstacle (quirk 1)
     const bool skip = !do_step || ((__ballot(act == 0xFF) & envmask) != 0);
-    const bool moved = mv && v != 0u && !skip;
+    const bool moved = mv && (v & 0x7Fu) != 0u && !skip;
     int dlt = (act & 2) ? 1 : pitch;  // 0: up, 1: down, 2: left, 3: right
     dlt = (act & 1) ? dlt : -dlt;
     const int nc = moved ? oc + dlt : oc;
-    if (has && !(MAPFX_ABLATE & 64)) dep[oc] = (unsigned char)((f_cur << 7) | (moved ? (uint32_t)act : 0x7Fu));
+    if (has && !(MAPFX_ABLATE & 64)) dep[oc] = (unsigned char)(moved ? (uint32_t)act : 0x7Fu);
     if (!(MAPFX_ABLATE & 16)) {
 #ifndef MAPFX_FULLW_ATOMICS
 #define MAPFX_FULLW_ATOMICS 1
@@ -1489,7 +1568,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
     } else {
       nbn = (x[1] & 0xFFu) | ((x[2] & 0xFFu) << 8) | ((xl & 0xFFu) << 16) | ((xr & 0xFFu) << 24);
     }
-    f_cur = dj >> 7;  // dep[nc] bit 7: static obstacle flag of the agent's new cell
     const bool dn_old = dn;
     const bool live = !skip && !(MAPFX_ABLATE & 128);
     if (live && nc == gcell) dn = true;          // :112-114 (goal reached)
@@ -1508,13 +1586,13 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
           const int rr_ = fastdiv(i, g.m_W4);
           const int cw = i - rr_ * wpr_out;
           const uint32_t vv = map32[((rr_ + g.P) * pitch + g.pl) / 4 + cw];
-          ((uint32_t*)outb)[i] = ((vv | 0x80808080u) - 0x01010101u) ^ 0x80808080u;  // c - 1
+          ((uint32_t*)outb)[i] = (((vv & 0x7F7F7F7Fu) | 0x80808080u) - 0x01010101u) ^ 0x80808080u;  // c - 1
         }
       } else {
         for (int i = ag; i < g.H * Wd; i += L) {
           const int rr_ = fastdiv(i, g.m_W);
           const int cc_ = i - rr_ * Wd;
-          ((int8_t*)outb)[i] = (int8_t)((int)map[(rr_ + g.P) * pitch + cc_ + g.pl] - 1);
+          ((int8_t*)outb)[i] = (int8_t)((int)(map[(rr_ + g.P) * pitch + cc_ + g.pl] & 0x7F) - 1);
         }
       }
     }
@@ -1528,7 +1606,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
     q_oc = oc;
     q_nc = nc;
     q_act = act;
-    q_pre = (int)v - 1 + (int)(dj >> 7);  // pre-step occupants of cand (moved lanes)
+    q_pre = (int)(v & 0x7Fu) - 1 + (int)(v >> 7);  // pre-step occupants of cand (moved lanes)
     q_dj = dj;
     q_nb = nbn;
     q_moved = moved;
@@ -1555,7 +1633,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
       if (has) {
         nb = (uint32_t)map[cur - pitch] | ((uint32_t)map[cur + pitch] << 8) |
              ((uint32_t)map[cur - 1] << 16) | ((uint32_t)map[cur + 1] << 24);
-        f_cur = (uint32_t)dep[cur] >> 7;
       }
     }
     STAMP(4);
@@ -1595,6 +1672,11 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
     if (a.steps) a.steps[oa] = st;
   }
   if (env_ok && ag == 0) a.t[env] = tcur;
+  PSTAMP(4);
+#ifdef MAPFX_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  PSTAMP(5);
+#endif
 #ifdef MAPFX_CLOCKS
   __builtin_amdgcn_s_waitcnt(0);
   if (lane64 == 0 && blockIdx.x < 32768) g_clk[8 * blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
@@ -1872,7 +1954,7 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   }
   const int cpw = 4 / es;  // cells per u32 word
   const int pl = round_up(P, cpw);
-  const int pitch = round_up(pl + c.W + P, cpw);
+  const int pitch = round_up(pl + c.W + P, 8 / es);  // rows 8-byte aligned (ds_write_b64 builds)
   const int rows = c.H + 2 * P;
 
   g.H = c.H;
@@ -1957,13 +2039,14 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     const int EPW = 64 / L;
     g.EPW = EPW;
     g.wv_bits_env_bytes = round_up(g.bits_words * 4 + 4, 16);
+    g.wv_fast = (c.W <= 64 && g.wpr <= MAPFX_FAST_WPR && (g.wpr & 1) == 0 && pl >= 1 && pl <= 32) ? 1 : 0;
     int o = 0;
     g.wv_off_map = o;
     o += EPW * g.map_env_bytes;
     g.wv_off_dep = o;
     o += EPW * g.map_env_bytes;
     g.wv_off_bits = o;
-    o += EPW * g.wv_bits_env_bytes;
+    o += g.wv_fast ? 0 : EPW * g.wv_bits_env_bytes;  // the fast build reads the bitmap from global
     // rew rows: N doubles rounded up to 2 (16 B), +2 doubles so the 4 envs of a wave
     // start on different banks
     g.wv_rew_row = (N + 1) / 2 * 2 + ((((N + 1) / 2 * 2) % 16) == 0 ? 2 : 0);

@@ -546,7 +546,9 @@ def run_partial(args, dist, rank, world, local):
 
 class RandomAvailMAC:
     """select_actions: uniform over each agent's available actions, on the device
-    (the shape of epsilon-greedy at epsilon = 1, action_selectors.py:65-69)."""
+    (the distribution of epsilon-greedy's random branch at epsilon = 1,
+    action_selectors.py:65-69: Categorical over the avail mask), sampled as the
+    argmax of uniform noise on the available actions (3 launches, no sync)."""
 
     def __init__(self, seed=0):
         self.gen = None
@@ -556,15 +558,12 @@ class RandomAvailMAC:
         pass
 
     def select_actions(self, batch, t_ep, t_env, bs, test_mode=False):
-        idx = torch.as_tensor(bs, dtype=torch.long, device=batch.device)
-        avail = batch["avail_actions"][idx, t_ep].float()
+        avail = batch["avail_actions"][bs, t_ep]
         if self.gen is None:
             self.gen = torch.Generator(device=avail.device)
             self.gen.manual_seed(self.seed)
-        n = avail.shape[0] * avail.shape[1]
-        if n == 0:
-            return torch.zeros(avail.shape[:2], dtype=torch.long, device=avail.device)
-        return torch.multinomial(avail.view(n, -1), 1, generator=self.gen).view(avail.shape[:2])
+        noise = torch.rand(avail.shape, generator=self.gen, device=avail.device)
+        return torch.argmax(noise * avail, dim=-1)
 
 
 def run_runner(args, dist, rank, world, local):
@@ -586,7 +585,7 @@ def run_runner(args, dist, rank, world, local):
     rargs = types.SimpleNamespace(env="marl_partial", batch_size_run=B, device="cuda:%d" % local,
                                   env_args=ea, episode_batch_cls=DeviceEpisodeBatch,
                                   test_nepisode=B, runner_log_interval=1 << 62)
-    runner = ParallelRunner(rargs, None, instance_fn=lambda e: (inst["init_pos"][e], inst["goals"][e]))
+    runner = ParallelRunner(rargs, None, instance_fn=lambda ep: (inst["init_pos"], inst["goals"]))
     info = runner.get_env_info()
     scheme = {"state": {"vshape": info["state_shape"]},
               "obs": {"vshape": info["obs_shape"], "group": "agents"},
@@ -594,7 +593,9 @@ def run_runner(args, dist, rank, world, local):
               "avail_actions": {"vshape": (info["n_actions"],), "group": "agents",
                                 "dtype": torch.int},
               "reward": {"vshape": (1,)}, "terminated": {"vshape": (1,), "dtype": torch.uint8}}
-    runner.setup(scheme, {"agents": N}, None, RandomAvailMAC(seed=rank))
+    from mapfx.episode import OneHot
+    runner.setup(scheme, {"agents": N}, {"actions": ("actions_onehot", [OneHot(out_dim=5)])},
+                 RandomAvailMAC(seed=rank))   # PyMARL's preprocess (run.py): one-hot actions
     runs = max(1, args.steps // info["episode_limit"])
     for _ in range(max(1, args.warmup // info["episode_limit"])):
         runner.run()

@@ -1,0 +1,265 @@
+// runner.hip — MI355X (gfx950) episode writes of the batched ParallelRunner
+// (include/mapfx_runner.h).
+//
+// The reference's runner loop (MARL-curve-main/src/runners/parallel_runner.py:91-173)
+// moves every env's transition through a Pipe and a Python list into PyMARL's
+// EpisodeBatch (components/episode_buffer.py:100-134).  These kernels write the
+// same rows from the batched env's device outputs into the EpisodeBatch tensors
+// and keep the runner's bookkeeping (running envs, the MAC's `bs` list, returns,
+// lengths, env-step count) on the device, so a runner step needs no host sync.
+//
+// Byte-moving work only (HBM-bound): one workgroup per env copies the env's
+// N x D float observation row with coalesced dword stores; the `bs` compaction is
+// one workgroup's prefix scan.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include "internal.h"
+#include "mapfx.h"
+#include "mapfx_runner.h"
+
+namespace {
+
+constexpr int RB = 256;  // threads of a row-copy workgroup
+
+int err(int code, const char* msg) { return mapfx_internal_error(code, msg); }
+
+int launch_ok(const char* what) {
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? MAPFX_OK : err(MAPFX_EHIP, what);
+}
+
+// obs / state / avail_actions (+ filled = 1) of env b into time row t
+__device__ inline void write_pre(const mapfx_runner_state& rs, const mapfx_partial_out& o,
+                                 const mapfx_episode_rows& r, int b, int t) {
+  const int ND = rs.N * rs.D;
+  if (r.obs) {  // U loads in flight per thread before the stores (restrict: no alias stalls)
+    const float* __restrict__ src = o.obs + (int64_t)b * ND;
+    float* __restrict__ dst = r.obs + (int64_t)b * r.obs_sb + (int64_t)t * r.obs_st;
+    constexpr int U = 8;
+    for (int base = 0; base < ND; base += RB * U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = base + u * RB + (int)threadIdx.x;
+        v[u] = i < ND ? src[i] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = base + u * RB + (int)threadIdx.x;
+        if (i < ND) dst[i] = v[u];
+      }
+    }
+  }
+  if (r.state && threadIdx.x < 3)
+    r.state[(int64_t)b * r.state_sb + (int64_t)t * r.state_st + threadIdx.x] = o.state[(int64_t)b * 3 + threadIdx.x];
+  if (r.avail) {  // 5-bit mask -> [N][5] int32 (get_avail_actions, marl_partial.py:389-433)
+    int32_t* dst = r.avail + (int64_t)b * r.avail_sb + (int64_t)t * r.avail_st;
+    for (int i = threadIdx.x; i < rs.N * 5; i += blockDim.x) {
+      const int n = i / 5, k = i - 5 * n;
+      dst[i] = (o.avail[(int64_t)b * rs.N + n] >> k) & 1;
+    }
+  }
+  if (r.filled && threadIdx.x == 0) r.filled[(int64_t)b * r.filled_sb + (int64_t)t * r.filled_st] = 1;
+}
+
+__global__ void __launch_bounds__(RB) runner_begin_kernel(mapfx_runner_state rs, mapfx_partial_out o,
+                                                          mapfx_episode_rows r) {
+  const int b = blockIdx.x;
+  write_pre(rs, o, r, b, 0);  // reset(): update(pre_transition_data, ts=0) (:62-76), all envs
+  if (threadIdx.x == 0) {
+    rs.alive[b] = 1;
+    rs.alive_prev[b] = 1;
+    rs.bs[b] = b;
+    rs.ep_return[b] = 0.0;
+    rs.ep_length[b] = 0;
+    if (b == 0) {
+      rs.counts[0] = rs.B;
+      rs.counts[1] = rs.B;
+      rs.env_steps[0] = 0;
+    }
+  }
+  for (int n = threadIdx.x; n < rs.N; n += blockDim.x) rs.env_actions[(int64_t)b * rs.N + n] = 4;
+}
+
+__device__ inline int64_t load_act(const void* p, int dtype, int64_t i) {
+  if (dtype == MAPFX_I8) return ((const int8_t*)p)[i];
+  if (dtype == MAPFX_I32) return ((const int32_t*)p)[i];
+  return ((const int64_t*)p)[i];
+}
+
+// update({"actions": actions.unsqueeze(1)}, bs=envs_not_terminated, ts) (:104-110) and
+// the OneHot preprocess (components/transforms.py) of the same rows
+__global__ void runner_actions_kernel(mapfx_runner_state rs, const void* acts, int dtype,
+                                      int64_t row_stride, int ts, mapfx_episode_rows r) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = (int)(i / rs.N), n = (int)(i - (int64_t)j * rs.N);
+  if (j >= rs.counts[0]) return;
+  const int64_t b = rs.bs[j];
+  const int64_t a = load_act(acts, dtype, (int64_t)j * row_stride + n);
+  if (r.actions) r.actions[b * r.actions_sb + (int64_t)ts * r.actions_st + n] = a;
+  if (r.onehot) {
+    float* oh = r.onehot + b * r.onehot_sb + (int64_t)ts * r.onehot_st + (int64_t)n * 5;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) oh[k] = (a == k) ? 1.0f : 0.0f;
+  }
+  // the env receives only the envs that have not terminated (:116-121); the others
+  // are never stepped again, whatever env_actions holds for them
+  rs.env_actions[b * rs.N + n] = (int8_t)((a < -128 || a > 127) ? -1 : a);
+}
+
+// receive loop of one step (:125-173) for every env still running
+__global__ void __launch_bounds__(RB) runner_post_kernel(mapfx_runner_state rs, const uint8_t* term,
+                                                         mapfx_partial_out o, int ts,
+                                                         mapfx_episode_rows r) {
+  const int b = blockIdx.x;
+  const uint8_t live = rs.alive[b];
+  __syncthreads();  // every thread read alive[b] before thread 0 rewrites it
+  if (live) {
+    const double R = o.reward[b];
+    const uint8_t tn = term[b] ? 1 : 0;
+    if (threadIdx.x == 0) {
+      if (r.reward) r.reward[(int64_t)b * r.reward_sb + (int64_t)ts * r.reward_st] = (float)R;
+      // env_terminated = terminated and not info.get("episode_limit") (:146-150): MARL_PARTIAL's
+      // info has no "episode_limit" key
+      if (r.terminated) r.terminated[(int64_t)b * r.terminated_sb + (int64_t)ts * r.terminated_st] = tn;
+      rs.ep_return[b] = rs.ep_return[b] + R;
+      rs.ep_length[b] += 1;
+      rs.alive[b] = tn ? 0 : 1;   // (env_steps: counted by the compaction, no atomics here)
+    }
+    if (ts + 1 < r.max_t) write_pre(rs, o, r, b, ts + 1);
+  }
+  if (threadIdx.x == 0) rs.alive_prev[b] = live;
+}
+
+// envs_not_terminated (:123) for the next MAC call: ascending indices of alive_prev,
+// padded with the first one (so a MAC indexing rows by `bs` only sees running envs);
+// counts = {len(bs), number alive}.  One workgroup: per-thread chunk counts, scan.
+constexpr int CT = 1024;
+__global__ void __launch_bounds__(CT) runner_compact_kernel(mapfx_runner_state rs, int32_t* counts_out) {
+  __shared__ int part[CT];
+  __shared__ int alive_part[CT];
+  const int chunk = (rs.B + CT - 1) / CT;
+  const int lo = threadIdx.x * chunk, hi = min(rs.B, lo + chunk);
+  int c = 0, ca = 0;
+  for (int b = lo; b < hi; ++b) {
+    c += rs.alive_prev[b] ? 1 : 0;
+    ca += rs.alive[b] ? 1 : 0;
+  }
+  part[threadIdx.x] = c;
+  alive_part[threadIdx.x] = ca;
+  __syncthreads();
+  for (int off = 1; off < CT; off <<= 1) {  // inclusive scan (Hillis-Steele)
+    const int v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    const int va = threadIdx.x >= off ? alive_part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    alive_part[threadIdx.x] += va;
+    __syncthreads();
+  }
+  int o = part[threadIdx.x] - c;
+  for (int b = lo; b < hi; ++b)
+    if (rs.alive_prev[b]) rs.bs[o++] = b;
+  const int total = part[CT - 1];
+  __syncthreads();  // bs[0] written
+  const int64_t first = total > 0 ? rs.bs[0] : 0;
+  for (int j = total + threadIdx.x; j < rs.B; j += CT) rs.bs[j] = first;
+  if (threadIdx.x == 0) {
+    rs.counts[0] = total;
+    rs.counts[1] = alive_part[CT - 1];
+    rs.env_steps[0] += total;  // the envs stepped this step: env_steps_this_run (:142)
+    if (counts_out) {  // possibly pinned host memory
+      counts_out[0] = total;
+      counts_out[1] = alive_part[CT - 1];
+    }
+  }
+}
+
+int check_rs(const mapfx_runner_state* rs) {
+  if (!rs || rs->B < 0 || rs->N < 1 || rs->D < 0 || !rs->alive || !rs->alive_prev || !rs->bs ||
+      !rs->counts || !rs->ep_return || !rs->ep_length || !rs->env_steps || !rs->env_actions)
+    return err(MAPFX_EINVAL, "runner state: NULL field or bad B/N/D");
+  return MAPFX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mapfx_runner_begin(const mapfx_runner_state* rs, const mapfx_partial_out* out,
+                       const mapfx_episode_rows* rows, void* stream) {
+  int rc = check_rs(rs);
+  if (rc) return rc;
+  if (!out || !rows || !out->obs || !out->state || !out->avail)
+    return err(MAPFX_EINVAL, "runner_begin: NULL out / rows");
+  if (rs->B == 0) return MAPFX_OK;
+  hipLaunchKernelGGL(runner_begin_kernel, dim3(rs->B), dim3(RB), 0, (hipStream_t)stream, *rs, *out, *rows);
+  return launch_ok("runner_begin_kernel launch");
+}
+
+int mapfx_runner_actions(const mapfx_runner_state* rs, const void* actions, int32_t action_dtype,
+                         int64_t row_stride, int32_t ts, const mapfx_episode_rows* rows,
+                         void* stream) {
+  int rc = check_rs(rs);
+  if (rc) return rc;
+  if (!actions || !rows) return err(MAPFX_EINVAL, "runner_actions: NULL actions / rows");
+  if (action_dtype < MAPFX_I8 || action_dtype > MAPFX_I64) return err(MAPFX_EINVAL, "runner_actions: bad dtype");
+  if (ts < 0 || ts >= rows->max_t) return err(MAPFX_EINVAL, "runner_actions: ts outside the batch");
+  const int64_t total = (int64_t)rs->B * rs->N;
+  if (total == 0) return MAPFX_OK;
+  hipLaunchKernelGGL(runner_actions_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, *rs, actions, (int)action_dtype, row_stride, (int)ts, *rows);
+  return launch_ok("runner_actions_kernel launch");
+}
+
+int mapfx_runner_post(const mapfx_runner_state* rs, const uint8_t* terminated,
+                      const mapfx_partial_out* out, int32_t ts, int32_t* counts_out,
+                      const mapfx_episode_rows* rows, void* stream) {
+  int rc = check_rs(rs);
+  if (rc) return rc;
+  if (!terminated || !out || !rows || !out->reward || !out->obs || !out->state || !out->avail)
+    return err(MAPFX_EINVAL, "runner_post: NULL terminated / out / rows");
+  if (ts < 0 || ts >= rows->max_t) return err(MAPFX_EINVAL, "runner_post: ts outside the batch");
+  if (rs->B == 0) return MAPFX_OK;
+  hipLaunchKernelGGL(runner_post_kernel, dim3(rs->B), dim3(RB), 0, (hipStream_t)stream, *rs, terminated,
+                     *out, (int)ts, *rows);
+  if ((rc = launch_ok("runner_post_kernel launch"))) return rc;
+  hipLaunchKernelGGL(runner_compact_kernel, dim3(1), dim3(CT), 0, (hipStream_t)stream, *rs, counts_out);
+  return launch_ok("runner_compact_kernel launch");
+}
+
+int mapfx_runner_step(mapfx_partial_t* h, const mapfx_partial_state* st, const mapfx_partial_out* out,
+                      const mapfx_runner_state* rs, const void* actions, int32_t action_dtype,
+                      int64_t row_stride, int32_t ts, int32_t* counts_out,
+                      const mapfx_episode_rows* rows, void* stream) {
+  int rc = mapfx_runner_actions(rs, actions, action_dtype, row_stride, ts, rows, stream);
+  if (rc) return rc;
+  if ((rc = mapfx_partial_step(h, st, rs->env_actions, MAPFX_I8, out, stream))) return rc;
+  return mapfx_runner_post(rs, st->terminated, out, ts, counts_out, rows, stream);
+}
+
+int mapfx_host_ring_alloc(int32_t n, int32_t** host_ptr, int32_t** dev_ptr) {
+  if (n < 1 || !host_ptr || !dev_ptr) return err(MAPFX_EINVAL, "host_ring_alloc: bad arguments");
+  *host_ptr = nullptr;
+  *dev_ptr = nullptr;
+  void* p = nullptr;
+  if (hipHostMalloc(&p, sizeof(int32_t) * (size_t)n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    return err(MAPFX_ENOMEM, "hipHostMalloc (mapped, coherent) failed");
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    (void)hipHostFree(p);
+    return err(MAPFX_EHIP, "hipHostGetDevicePointer failed");
+  }
+  memset(p, 0, sizeof(int32_t) * (size_t)n);
+  *host_ptr = (int32_t*)p;
+  *dev_ptr = (int32_t*)d;
+  return MAPFX_OK;
+}
+
+void mapfx_host_ring_free(int32_t* host_ptr) {
+  if (host_ptr) (void)hipHostFree(host_ptr);
+}
+
+}  // extern "C"

@@ -91,7 +91,20 @@ EXPORTS = ("mapfx_abi_version", "mapfx_last_error", "mapfx_map_stride", "mapfx_o
            "mapfx_partial_create", "mapfx_partial_destroy", "mapfx_partial_obs_dim",
            "mapfx_partial_goal_dist", "mapfx_partial_reset", "mapfx_partial_step",
            "mapfx_partial_observe", "mapfx_primal_create", "mapfx_primal_destroy",
-           "mapfx_primal_act")
+           "mapfx_primal_act", "mapfx_runner_begin", "mapfx_runner_actions", "mapfx_runner_post",
+           "mapfx_runner_step", "mapfx_host_ring_alloc", "mapfx_host_ring_free")
+
+
+class ERows(ctypes.Structure):  # include/mapfx_runner.h mapfx_episode_rows
+    _fields_ = [("max_t", c_i32)] + [f for k in ("obs", "state", "avail", "actions", "onehot",
+                                                 "reward", "terminated", "filled")
+                                     for f in ((k, c_vp), (k + "_sb", c_i64), (k + "_st", c_i64))]
+
+
+class RState(ctypes.Structure):  # include/mapfx_runner.h mapfx_runner_state
+    _fields_ = [("B", c_i32), ("N", c_i32), ("D", c_i32)] + [
+        (k, c_vp) for k in ("alive", "alive_prev", "bs", "counts", "ep_return", "ep_length",
+                            "env_steps", "env_actions")]
 
 
 class MapfxError(RuntimeError):
@@ -129,6 +142,13 @@ def _load():
         "mapfx_primal_create": (c_i32, [P(QCfg), P(c_vp)]),
         "mapfx_primal_destroy": (None, [c_vp]),
         "mapfx_primal_act": (c_i32, [c_vp, P(QState), c_vp, c_vp, c_i32, P(QOut), c_vp]),
+        "mapfx_runner_begin": (c_i32, [P(RState), P(POut), P(ERows), c_vp]),
+        "mapfx_runner_actions": (c_i32, [P(RState), c_vp, c_i32, c_i64, c_i32, P(ERows), c_vp]),
+        "mapfx_runner_post": (c_i32, [P(RState), c_vp, P(POut), c_i32, c_vp, P(ERows), c_vp]),
+        "mapfx_runner_step": (c_i32, [c_vp, P(PState), P(POut), P(RState), c_vp, c_i32, c_i64, c_i32,
+                                      c_vp, P(ERows), c_vp]),
+        "mapfx_host_ring_alloc": (c_i32, [c_i32, P(c_vp), P(c_vp)]),
+        "mapfx_host_ring_free": (None, [c_vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

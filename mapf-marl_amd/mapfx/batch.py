@@ -40,7 +40,7 @@ class MapfGridBatch:
 
     def __init__(self, init_pos, goals, grids=None, bits=None, hw=None, episode_limit=10000,
                  step_reward=-0.01, collide_reward=-10, obs=("full",), window=5,
-                 primal_size=10, device=None, env_offset=0, track_steps=True):
+                 primal_size=10, device=None, env_offset=0, track_steps=True, packed=False):
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("MapfGridBatch runs on a HIP device only (got %s)" % self.device)
@@ -91,14 +91,34 @@ class MapfGridBatch:
         self.bits = torch.as_tensor(bits).to(dev)
         self.init_pos = init_pos.to(dev).contiguous()
         self.goal = goals.to(dev).contiguous()
-        self.pos = self.init_pos.clone()
-        self.done = torch.zeros((self.E, self.N), dtype=torch.uint8, device=dev)
-        self.t = torch.zeros((self.E,), dtype=torch.int32, device=dev)
-        self.steps = torch.zeros((self.E, self.N), dtype=torch.int32, device=dev) \
-            if track_steps else None
-        self.err = torch.zeros((1,), dtype=torch.int32, device=dev)
         self.obs_elem = torch.int8 if lib.mapfx_obs_elem_size(self.N) == 1 else torch.int16
-        self.out = self._alloc_out(None)
+        self.err = torch.zeros((1,), dtype=torch.int32, device=dev)
+        # `packed`: the mutable state and every per-step output are views of ONE flat
+        # device buffer (mapfx.dist.ChunkLayout), so a host mirror of all of it is a
+        # single copy (the drop-in env pulls a step's results with one sync).
+        spec = {"pos": ((self.E, self.N, 2), torch.int32), "done": ((self.E, self.N), torch.uint8),
+                "t": ((self.E,), torch.int32), "err": ((1,), torch.int32)}
+        if track_steps:
+            spec["steps"] = ((self.E, self.N), torch.int32)
+        spec.update(self.out_spec(None))
+        self.packed = bool(packed)
+        if self.packed:
+            from .dist import ChunkLayout
+            self._layout = ChunkLayout(spec)
+            self._flat = self._layout.alloc(dev)
+            v = self._layout.views(self._flat)
+            self.pos, self.done, self.t, self.err = v["pos"], v["done"], v["t"], v["err"]
+            self.pos.copy_(self.init_pos)
+            self.steps = v.get("steps")
+            self.out = {k: v[k] for k in self.out_spec(None)}
+        else:
+            self._layout = self._flat = None
+            self.pos = self.init_pos.clone()
+            self.done = torch.zeros((self.E, self.N), dtype=torch.uint8, device=dev)
+            self.t = torch.zeros((self.E,), dtype=torch.int32, device=dev)
+            self.steps = torch.zeros((self.E, self.N), dtype=torch.int32, device=dev) \
+                if track_steps else None
+            self.out = self._alloc_out(None)
         self._out_cache = {}          # outputs selection -> Out struct over self.out
         self._traj_cache = {}         # (id(traj), outputs) -> Out struct over a trajectory
         self._dev_index = self.device.index if self.device.index is not None \
@@ -274,6 +294,20 @@ class MapfGridBatch:
             check(lib.mapfx_gen_actions(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(t0), int(T),
                                         ptr(out), _stream_handle()), "mapfx_gen_actions")
         return out
+
+    def host_mirror(self):
+        """Pinned host copy of the packed buffer and its typed views (packed=True)."""
+        if not self.packed:
+            raise RuntimeError("host_mirror needs MapfGridBatch(..., packed=True)")
+        flat = torch.empty(self._layout.nbytes, dtype=torch.uint8, pin_memory=True)
+        return flat, self._layout.views(flat)
+
+    def pull(self, host_flat):
+        """Copy state + outputs into `host_flat` (host_mirror) and wait for it: the
+        one synchronisation of a drop-in step."""
+        host_flat.copy_(self._flat, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return host_flat
 
     def check_err(self):
         """Raise AssertionError like the reference (:91-92) if an env got an

@@ -90,8 +90,14 @@ class MAPF_GRID(MultiAgentEnv):
         self._batch = MapfGridBatch(init, goals, grids=self._grid[None],
                                     episode_limit=self.episode_limit,
                                     step_reward=self._step_rew, collide_reward=self._collide_rew,
-                                    obs=("full",), device=self._device)
+                                    obs=("full",), device=self._device, packed=True)
         self._built_from = (init.tobytes(), goals.tobytes())
+        # one pinned host mirror of state + outputs (one D2H copy per step) and a
+        # pinned action row -> device row (no pageable copies on the step path)
+        self._host_flat, self._host = self._batch.host_mirror()
+        self._act_host = torch.empty((1, self._n_agents), dtype=torch.int8, pin_memory=True)
+        self._act_dev = torch.empty((1, self._n_agents), dtype=torch.int8,
+                                    device=self._batch.device)
 
     # ---------------------------------------------------------------- plugin API
     def reset(self):
@@ -115,10 +121,11 @@ class MAPF_GRID(MultiAgentEnv):
         return self.get_obs()
 
     def _pull(self):
-        b = self._batch
-        o = b.out
-        self._occ = o["obs_full"][0].to(torch.int64).cpu().numpy()
-        self._avail_mask = o["avail"][0].cpu().numpy()
+        """The step's state and outputs -> host: ONE copy + ONE stream sync."""
+        self._batch.pull(self._host_flat)
+        h = self._host
+        self._occ = h["obs_full"][0].numpy().astype(np.int64)
+        self._avail_mask = h["avail"][0].numpy()
 
     def step(self, agents_action):
         """:85-141 — returns (sum(rewards), self._agent_dones (aliased), info)."""
@@ -129,16 +136,17 @@ class MAPF_GRID(MultiAgentEnv):
         assert len(agents_action) == self._n_agents                              # :91
         assert all([action_i in ACTION_MEANING.keys() for action_i in agents_action])  # :92
         done_pre = list(self._agent_dones)
-        acts = torch.as_tensor(np.asarray([int(a) for a in agents_action], dtype=np.int8)[None])
+        self._act_host.numpy()[0] = [int(a) for a in agents_action]
+        self._act_dev.copy_(self._act_host, non_blocking=True)
         b = self._batch
-        b.step(acts)
-        o = b.out
-        R = float(o["reward"][0].item())
-        pos = b.pos[0].cpu().numpy()
-        done = b.done[0].cpu().numpy()
-        node = o["node"][0].cpu().numpy()
-        edge = o["edge"][0].cpu().numpy()
+        b.step(self._act_dev)
         self._pull()
+        h = self._host
+        R = float(h["reward"][0])
+        pos = h["pos"][0].numpy()
+        done = h["done"][0].numpy()
+        node = h["node"][0].numpy()
+        edge = h["edge"][0].numpy()
         self._step_count += 1
         for i in self.agents:
             if not done_pre[i]:

@@ -98,7 +98,11 @@ class MARL_PARTIAL_ENV(MultiAgentEnv):
         goals = np.array([self._agent_goal_pos], dtype=np.int32)
         if self._batch is None:
             self._batch = MarlPartialBatch(init, goals, grids=self._grid[None],
-                                           device=self._device, **self._params)
+                                           device=self._device, packed=True, **self._params)
+            self._host_flat, self._host = self._batch.host_mirror()
+            self._act_host = torch.empty((1, self._n_agents), dtype=torch.int8, pin_memory=True)
+            self._act_dev = torch.empty((1, self._n_agents), dtype=torch.int8,
+                                        device=self._batch.device)
         else:
             self._batch.set_agents(init, goals)
 
@@ -114,11 +118,13 @@ class MARL_PARTIAL_ENV(MultiAgentEnv):
         return self.get_obs()
 
     def _pull(self):
-        o = self._batch.out
-        self._obs = o["obs"][0].cpu().numpy()
-        self._state = o["state"][0].cpu().numpy()
-        self._avail_mask = o["avail"][0].cpu().numpy()
-        self._agent_positions = [tuple(int(v) for v in p) for p in self._batch.pos[0].cpu().numpy()]
+        """The step's state and outputs -> host: ONE copy + ONE stream sync."""
+        self._batch.pull(self._host_flat)
+        h = self._host
+        self._obs = h["obs"][0].numpy().copy()
+        self._state = h["state"][0].numpy().copy()
+        self._avail_mask = h["avail"][0].numpy().copy()
+        self._agent_positions = [tuple(int(v) for v in p) for p in h["pos"][0].numpy()]
 
     def agent_pos(self, agent_id):
         assert -1 < agent_id < self._n_agents
@@ -130,13 +136,14 @@ class MARL_PARTIAL_ENV(MultiAgentEnv):
             agents_action = agents_action.detach().cpu().numpy()
         assert len(agents_action) == self._n_agents                              # :173
         assert all([action_i in ACTION_MEANING.keys() for action_i in agents_action])  # :174
-        acts = torch.as_tensor(np.asarray([int(a) for a in agents_action], dtype=np.int8)[None])
-        b = self._batch
-        b.step(acts)
-        R = float(b.out["reward"][0].item())
-        self._step_count += 1
-        self._terminated = bool(b.terminated[0].item())
+        self._act_host.numpy()[0] = [int(a) for a in agents_action]
+        self._act_dev.copy_(self._act_host, non_blocking=True)
+        self._batch.step(self._act_dev)
         self._pull()
+        h = self._host
+        R = float(h["reward"][0])
+        self._step_count += 1
+        self._terminated = bool(h["terminated"][0])
         return R, self._terminated, {'_step_count': self._step_count}
 
     def get_obs(self):
@@ -184,4 +191,4 @@ class MARL_PARTIAL_ENV(MultiAgentEnv):
                 "episode_limit": self.episode_limit}
 
     def episode_done(self):
-        return bool(self._batch.done[0].all().item())
+        return bool(self._host["done"][0].all())

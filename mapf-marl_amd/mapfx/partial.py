@@ -31,7 +31,7 @@ class MarlPartialBatch:
     (nonzero = obstacle) or `bits` [E|1, map_stride]; init_pos / goals [E, N, 2]."""
 
     def __init__(self, init_pos, goals, grids=None, bits=None, hw=None, device=None, env_offset=0,
-                 **params):
+                 packed=False, **params):
         unknown = set(params) - set(DEFAULTS)
         if unknown:
             raise TypeError("unknown MARL_PARTIAL_ENV parameters: %s" % sorted(unknown))
@@ -77,26 +77,41 @@ class MarlPartialBatch:
             check(lib.mapfx_partial_create(ctypes.byref(cfg), ctypes.byref(h)),
                   "mapfx_partial_create")
         self._h = h
+        self._dev_index = self.device.index if self.device.index is not None \
+            else torch.cuda.current_device()
         self.obs_dim = int(lib.mapfx_partial_obs_dim(h))
         E, N, dev = self.E, self.N, self.device
         z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
         self.bits = torch.as_tensor(bits).to(dev)
         self.init_pos = torch.as_tensor(init_pos).to(dev).contiguous()
         self.goal = torch.as_tensor(goals).to(dev).contiguous()
-        self.pos = self.init_pos.clone()
+        # `packed`: what the drop-in env reads after a step (positions, flags and the
+        # outputs) are views of ONE flat buffer, pulled to the host with one copy
+        spec = {"pos": ((E, N, 2), torch.int32), "done": ((E, N), torch.uint8),
+                "terminated": ((E,), torch.uint8), "t": ((E,), torch.int32),
+                "err": ((1,), torch.int32), "reward": ((E,), torch.float64),
+                "obs": ((E, N, self.obs_dim), torch.float32), "state": ((E, 3), torch.float32),
+                "avail": ((E, N), torch.uint8)}
+        self.packed = bool(packed)
+        if self.packed:
+            from .dist import ChunkLayout
+            self._layout = ChunkLayout(spec)
+            self._flat = self._layout.alloc(dev)
+            v = self._layout.views(self._flat)
+        else:
+            self._layout = self._flat = None
+            v = {k: z(shape, dt) for k, (shape, dt) in spec.items()}
+        self.pos, self.done, self.terminated, self.t, self.err = (
+            v["pos"], v["done"], v["terminated"], v["t"], v["err"])
+        self.pos.copy_(self.init_pos)
         self.steps = z((E, N), torch.int32)
         self.at_goal = z((E, N), torch.uint8)
-        self.done = z((E, N), torch.uint8)
         self.goal_cost = z((E, N), torch.int32)
         self.node = z((E, N), torch.uint8)
         self.edge = z((E, N), torch.int32)
-        self.t = z((E,), torch.int32)
-        self.terminated = z((E,), torch.uint8)
         self.total_coll = z((E,), torch.int32)
         self.goal_dist = z((E, N, self.H * self.W), torch.int16)
-        self.err = z((1,), torch.int32)
-        self.out = {"reward": z((E,), torch.float64), "obs": z((E, N, self.obs_dim), torch.float32),
-                    "state": z((E, 3), torch.float32), "avail": z((E, N), torch.uint8)}
+        self.out = {k: v[k] for k in ("reward", "obs", "state", "avail")}
         self._state = _abi.PState(
             pos=ptr(self.pos), goal=ptr(self.goal), init_pos=ptr(self.init_pos),
             steps=ptr(self.steps), at_goal=ptr(self.at_goal), done=ptr(self.done),
@@ -118,6 +133,9 @@ class MarlPartialBatch:
             self._h = None
 
     def _call(self, fn, *args):
+        """Run a C-ABI call with self.device current (no context switch when it already is)."""
+        if torch.cuda.current_device() == self._dev_index:
+            return fn(*args, torch.cuda.current_stream().cuda_stream)
         with torch.cuda.device(self.device):
             return fn(*args, torch.cuda.current_stream().cuda_stream)
 
@@ -167,6 +185,19 @@ class MarlPartialBatch:
         check(self._call(lib.mapfx_partial_step, self._h, ctypes.byref(self._state), ptr(a),
                          _DTYPES[a.dtype], ctypes.byref(self._out)), "mapfx_partial_step")
         return self.out
+
+    def host_mirror(self):
+        """Pinned host copy of the packed buffer and its typed views (packed=True)."""
+        if not self.packed:
+            raise RuntimeError("host_mirror needs MarlPartialBatch(..., packed=True)")
+        flat = torch.empty(self._layout.nbytes, dtype=torch.uint8, pin_memory=True)
+        return flat, self._layout.views(flat)
+
+    def pull(self, host_flat):
+        """Copy the packed buffer into `host_flat` and wait for it (one sync)."""
+        host_flat.copy_(self._flat, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return host_flat
 
     def check_err(self):
         e = int(self.err.item())

@@ -4,21 +4,37 @@ Same public surface as MARL-curve-main/src/runners/parallel_runner.py
 (`ParallelRunner.__init__(args, logger)`, `setup(scheme, groups, preprocess, mac)`,
 `get_env_info`, `reset`, `run(test_mode)`, `close_env`, `save_replay`, the
 `t_env` counter and the return / stat logging), but the `batch_size_run` envs are
-one MarlPartialBatch on the GPU instead of one subprocess + Pipe each: no
-pickling, no numpy round trip, and `batch.update` receives device tensors.
+one MarlPartialBatch on the GPU instead of one subprocess + Pipe each, and a
+runner step is: the MAC's select_actions, then three device launches
+(include/mapfx_runner.h) -- actions rows, the env step, the step's rows straight
+into the EpisodeBatch tensors with the runner's bookkeeping (running envs, the
+MAC's `bs`, returns, lengths, env steps) kept on the device.  No per-step host
+synchronisation: the loop-exit test reads the count of running envs two steps
+late from a pinned ring (the reference stops one MAC call after the last env
+terminated, and that call is exactly the one the lag covers; see `run`).
 
-The EpisodeBatch the runner fills is whatever `setup` is given (PyMARL passes
-`components.episode_buffer.EpisodeBatch`); the runner only calls its constructor
-and `update(data, bs, ts, mark_filled)` exactly as the reference runner does
-(parallel_runner.py:62-76 reset, :91-173 run).
+The EpisodeBatch is whatever `setup` is given (PyMARL passes
+components.episode_buffer.EpisodeBatch); the runner writes its
+`data.transition_data` tensors (PyMARL's scheme: obs / state float32,
+avail_actions int32, actions int64 (+ actions_onehot float32 from the OneHot
+preprocess), reward float32, terminated uint8, filled int64) on the batch's device.
+
+Row semantics are the reference's (tests/golden/runner_*.npz were produced by the
+reference ParallelRunner itself), including its stale list: the MAC's `bs` and the
+actions row at step t cover the envs that were running before step t - 1.  The
+MAC gets `bs` as a device LongTensor of length B (ascending running env ids,
+padded with the first one), a form the reference EpisodeBatch / BasicMAC index
+with (episode_buffer.py:186-190).
 
 Per-env instances: every reset draws each env's scenario like
 MARL_PARTIAL_ENV.__setup_agent (:896-920: random.randint(1, 25) then
-random.sample of the scen lines), from a per-env `random.Random(seed + e)`
-stream (the reference's forked workers would all share one stream).
+random.sample of the scen lines), from a per-env `random.Random(seed + e)` stream
+(the reference's forked workers all share one stream and draw identical instances).
+`instance_fn(episode) -> (starts [B, N, 2], goals [B, N, 2])` overrides the draw.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import random
 from functools import partial
@@ -26,16 +42,36 @@ from functools import partial
 import numpy as np
 import torch
 
+from . import _abi
+from ._abi import MAPFX_I8, MAPFX_I32, MAPFX_I64, check, lib, ptr
 from .maps import load_map
 from .partial import MarlPartialBatch
+
+_ADT = {torch.int8: MAPFX_I8, torch.int32: MAPFX_I32, torch.int64: MAPFX_I64}
+_ROW_DTYPES = {"obs": torch.float32, "state": torch.float32, "avail_actions": torch.int32,
+               "actions": torch.int64, "actions_onehot": torch.float32, "reward": torch.float32,
+               "terminated": torch.uint8, "filled": torch.int64}
+_ROW_FIELDS = {"obs": "obs", "state": "state", "avail_actions": "avail", "actions": "actions",
+               "actions_onehot": "onehot", "reward": "reward", "terminated": "terminated",
+               "filled": "filled"}
+_RING = 4
+
+
+_SCEN_CACHE = {}
+
+
+def _scen_lines(path):
+    lines = _SCEN_CACHE.get(path)
+    if lines is None:
+        assert os.path.exists(path)
+        with open(path) as f:
+            lines = _SCEN_CACHE[path] = [row.rstrip() for row in f.readlines()][1:]
+    return lines
 
 
 def _scen_draw(rng, agents_path, n):
     """:896-920 with an explicit Random: (starts, goals) as (row, col)."""
-    path = agents_path + str(rng.randint(1, 25)) + ".scen"
-    assert os.path.exists(path)
-    with open(path) as f:
-        lines = [row.rstrip() for row in f.readlines()][1:]
+    lines = _scen_lines(agents_path + str(rng.randint(1, 25)) + ".scen")
     assert len(lines) > n
     starts, goals = [], []
     for line in rng.sample(lines, n):
@@ -59,17 +95,45 @@ class ParallelRunner:
         grid_path, self.agents_path = ea.pop("grid_file_path"), ea.pop("agents_path")
         for k in ("seed", "render", "debug", "visual", "output"):
             ea.pop(k, None)
-        self.device = torch.device(getattr(args, "device", "cuda"))
+        dev = torch.device(getattr(args, "device", "cuda"))
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
         self.grid = load_map(grid_path)
         seed = int(getattr(args, "seed", 0) or 0)
         self._rngs = [random.Random(seed + e) for e in range(self.batch_size)]
-        # instance_fn(env_index) -> (starts, goals) overrides the scen draw (tests)
         self._instance_fn = instance_fn
+        self._episode = 0
         starts, goals = self._draw()
         self.env = MarlPartialBatch(starts, goals, grids=self.grid[None], device=self.device, **ea)
+        self._loaded = (starts.tobytes(), goals.tobytes())
         self.env_info = {"state_shape": 3, "obs_shape": self.env.obs_dim, "n_actions": 5,
                          "n_agents": self.n_agents, "episode_limit": self.env.episode_limit}
         self.episode_limit = self.env_info["episode_limit"]
+        B, N, dev = self.batch_size, self.n_agents, self.device
+        z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
+        self._alive, self._alive_prev = z((B,), torch.uint8), z((B,), torch.uint8)
+        self._bs = z((B,), torch.int64)
+        self._counts = z((2,), torch.int32)
+        self._ep_return, self._ep_length = z((B,), torch.float64), z((B,), torch.int64)
+        self._env_steps = z((1,), torch.int64)
+        self._env_actions = torch.full((B, N), 4, dtype=torch.int8, device=dev)
+        self._rs = _abi.RState(B=B, N=N, D=self.env.obs_dim, alive=ptr(self._alive),
+                               alive_prev=ptr(self._alive_prev), bs=ptr(self._bs),
+                               counts=ptr(self._counts), ep_return=ptr(self._ep_return),
+                               ep_length=ptr(self._ep_length), env_steps=ptr(self._env_steps),
+                               env_actions=ptr(self._env_actions))
+        # counts {len(bs), running} of step k land in slot k % _RING of a mapped host
+        # buffer, written by the compaction kernel itself (no copy launch); the slot's
+        # event marks them final
+        hp, dp = ctypes.c_void_p(), ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib.mapfx_host_ring_alloc(2 * _RING, ctypes.byref(hp), ctypes.byref(dp)),
+                  "mapfx_host_ring_alloc")
+        self._ring_host = hp
+        host = np.ctypeslib.as_array(ctypes.cast(hp, ctypes.POINTER(ctypes.c_int32)),
+                                     shape=(_RING, 2))
+        self._ring = [(torch.cuda.Event(), host[i], dp.value + 8 * i) for i in range(_RING)]
         self.t = 0
         self.t_env = 0
         self.train_returns = []
@@ -79,13 +143,15 @@ class ParallelRunner:
         self.log_train_stats_t = -100000
 
     def _draw(self):
-        st, gl = [], []
-        for e in range(self.batch_size):
-            s, g = (self._instance_fn(e) if self._instance_fn else
-                    _scen_draw(self._rngs[e], self.agents_path, self.n_agents))
-            st.append(s)
-            gl.append(g)
-        return np.array(st, dtype=np.int32), np.array(gl, dtype=np.int32)
+        if self._instance_fn is not None:
+            st, gl = self._instance_fn(self._episode)
+        else:
+            st, gl = [], []
+            for e in range(self.batch_size):
+                s, g = _scen_draw(self._rngs[e], self.agents_path, self.n_agents)
+                st.append(s)
+                gl.append(g)
+        return np.asarray(st, dtype=np.int32), np.asarray(gl, dtype=np.int32)
 
     def setup(self, scheme, groups, preprocess, mac):
         device = getattr(self.args, "device", "cuda")
@@ -103,6 +169,12 @@ class ParallelRunner:
             cls = EpisodeBatch
         return cls
 
+    def __del__(self):
+        hp = getattr(self, "_ring_host", None)
+        if hp is not None and hp.value:
+            lib.mapfx_host_ring_free(hp)
+            self._ring_host = None
+
     def get_env_info(self):
         return self.env_info
 
@@ -112,76 +184,125 @@ class ParallelRunner:
     def close_env(self):
         pass
 
-    def _pre_transition(self, bs=None):
-        o = self.env.out
-        sel = (lambda x: x) if bs is None else (lambda x: x[bs])
-        return {"state": sel(o["state"]), "avail_actions": sel(self.env.avail_actions()),
-                "obs": sel(o["obs"])}
+    # ------------------------------------------------------------------ rows
+    def _rows(self, batch):
+        """mapfx_episode_rows over the batch's transition tensors (checked)."""
+        td = batch.data.transition_data
+        r = _abi.ERows(max_t=int(batch.max_seq_length))
+        B, N, D = self.batch_size, self.n_agents, self.env.obs_dim
+        shapes = {"obs": (N, D), "state": (3,), "avail_actions": (N, 5), "actions": (N, 1),
+                  "actions_onehot": (N, 5), "reward": (1,), "terminated": (1,), "filled": (1,)}
+        for key, field in _ROW_FIELDS.items():
+            t = td.get(key)
+            if t is None:
+                if key != "actions_onehot":
+                    raise KeyError("EpisodeBatch has no %r field" % key)
+                continue
+            if t.dtype != _ROW_DTYPES[key] or tuple(t.shape[2:]) != shapes[key] or \
+                    t.shape[0] != B or t.device != self.device:
+                raise ValueError("EpisodeBatch %r is %s %s on %s; the runner writes %s %s on %s"
+                                 % (key, t.dtype, tuple(t.shape), t.device, _ROW_DTYPES[key],
+                                    (B, r.max_t) + shapes[key], self.device))
+            inner = 1
+            for s in shapes[key]:
+                inner *= s
+            if t.stride(-1) != 1 or t.stride(1) < inner or (len(shapes[key]) > 1 and
+                                                             t.stride(2) != shapes[key][1]):
+                raise ValueError("EpisodeBatch %r rows are not contiguous" % key)
+            setattr(r, field, ptr(t))
+            setattr(r, field + "_sb", t.stride(0))
+            setattr(r, field + "_st", t.stride(1))
+        if "actions_onehot" in td:
+            pre = (self.preprocess or {}).get("actions")
+            tf = pre[1] if pre else []
+            if not (pre and pre[0] == "actions_onehot" and len(tf) == 1
+                    and type(tf[0]).__name__ == "OneHot" and getattr(tf[0], "out_dim", 5) == 5):
+                raise ValueError("actions_onehot must come from the OneHot(out_dim=5) preprocess")
+        return r
 
+    def _call(self, fn, *args):
+        return fn(*args, torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ------------------------------------------------------------------ loop
     def reset(self):
-        """:62-76: new batch, every env reset (instances re-drawn, :130), t = 0 data."""
+        """:62-76: new batch, every env reset (instances re-drawn, :130), row 0."""
         self.batch = self.new_batch()
         starts, goals = self._draw()
-        self.env.set_agents(starts, goals)
+        key = (starts.tobytes(), goals.tobytes())
+        if key != self._loaded:           # same instances: the BFS tables still hold
+            self.env.set_agents(starts, goals)
+            self._loaded = key
+        self._episode += 1
         self.env.reset()
-        self.batch.update(self._pre_transition(), ts=0)
+        self._erows = self._rows(self.batch)
+        check(self._call(lib.mapfx_runner_begin, ctypes.byref(self._rs),
+                         ctypes.byref(self.env._obs_out), ctypes.byref(self._erows)),
+              "mapfx_runner_begin")
         self.t = 0
         self.env_steps_this_run = 0
 
     def run(self, test_mode=False):
-        """:78-206 with the envs stepped as one batch on the device."""
+        """:78-206 with the envs stepped as one batch on the device.
+
+        Iteration k of the reference calls the MAC (bs = envs running before step
+        k - 1), writes the actions rows, then stops if no env is running after step
+        k - 1, else steps and writes the step's rows.  Here iteration k first
+        stops if no env was running after step k - 2 (pinned ring, two iterations
+        old: no wait in the steady state), which is the reference's stop one
+        iteration later; the one step that can run in between finds no running
+        env and writes nothing."""
         self.reset()
-        B, N = self.batch_size, self.n_agents
-        dev = self.device
-        episode_returns = torch.zeros(B, dtype=torch.float64, device=dev)
-        episode_lengths = torch.zeros(B, dtype=torch.int64, device=dev)
-        self.mac.init_hidden(batch_size=B)
-        terminated = torch.zeros(B, dtype=torch.bool, device=dev)
-        envs_not_terminated = list(range(B))
-        full_actions = torch.full((B, N), 4, dtype=torch.int64, device=dev)
+        self.mac.init_hidden(batch_size=self.batch_size)
+        r, rs, env = self._erows, ctypes.byref(self._rs), self.env
+        stream = torch.cuda.current_stream(self.device)
+        sh = stream.cuda_stream
+        fixed = (env._h, ctypes.byref(env._state), ctypes.byref(env._out), rs)
+        step = lib.mapfx_runner_step
+        k = 0
         while True:
-            actions = self.mac.select_actions(self.batch, t_ep=self.t, t_env=self.t_env,
-                                              bs=envs_not_terminated, test_mode=test_mode)
-            self.batch.update({"actions": actions.unsqueeze(1)}, bs=envs_not_terminated, ts=self.t,
-                              mark_filled=False)
-            # actions reach the envs of the list that have not terminated (:116-121); the
-            # list itself is refreshed only afterwards (:123), as in the reference
-            sel = torch.as_tensor(envs_not_terminated, dtype=torch.int64, device=dev)
-            full_actions.fill_(4)  # envs that are not stepped take "stay" (rows never written)
-            if len(envs_not_terminated):
-                full_actions[sel] = actions.to(dev).view(-1, N).to(torch.int64)
-            bs_idx = torch.nonzero(~terminated).flatten()
-            envs_not_terminated = bs_idx.tolist()
-            if bool(terminated.all()):
-                break
-            out = self.env.step(full_actions)
-            reward = out["reward"][bs_idx]
-            term_now = self.env.terminated[bs_idx].bool()
-            episode_returns[bs_idx] += reward
-            episode_lengths[bs_idx] += 1
-            if not test_mode:
-                self.env_steps_this_run += len(envs_not_terminated)
-            # env_terminated = terminated and not info["episode_limit"] (:147-150);
-            # MARL_PARTIAL's info carries no "episode_limit" key
-            self.batch.update({"reward": reward.unsqueeze(1),
-                               "terminated": term_now.unsqueeze(1)},
-                              bs=envs_not_terminated, ts=self.t, mark_filled=False)
-            terminated[bs_idx] = term_now
-            self.t += 1
-            self.batch.update(self._pre_transition(bs_idx), bs=envs_not_terminated, ts=self.t,
-                              mark_filled=True)
+            if k >= 2:   # no env running after step k - 2: the reference stopped at k - 1
+                ev, hc, _ = self._ring[(k - 2) % _RING]
+                ev.synchronize()
+                if int(hc[1]) == 0:
+                    break
+            actions = self.mac.select_actions(self.batch, t_ep=k, t_env=self.t_env, bs=self._bs,
+                                              test_mode=test_mode)
+            a = actions.reshape(self.batch_size, self.n_agents)
+            if a.device != self.device:
+                a = a.to(self.device)
+            if a.dtype not in _ADT:
+                a = a.to(torch.int64)
+            a = a.contiguous()
+            ev, _, dslot = self._ring[k % _RING]
+            rc = step(*fixed, a.data_ptr(), _ADT[a.dtype], a.stride(0), k, dslot, ctypes.byref(r), sh)
+            if rc:
+                check(rc, "mapfx_runner_step")
+            ev.record(stream)
+            k += 1
+        self.t = k
+        # the run's totals: one transfer at the end
+        env_steps = int(self._env_steps.item())
+        returns = self._ep_return.cpu().tolist()
+        lengths = self._ep_length.cpu()
+        self.env_steps_this_run = 0 if test_mode else env_steps
         if not test_mode:
-            self.t_env += self.env_steps_this_run
+            self.t_env += env_steps
         cur_stats = self.test_stats if test_mode else self.train_stats
         cur_returns = self.test_returns if test_mode else self.train_returns
         log_prefix = "test_" if test_mode else ""
-        cur_stats["n_episodes"] = B + cur_stats.get("n_episodes", 0)
-        cur_stats["ep_length"] = int(episode_lengths.sum().item()) + cur_stats.get("ep_length", 0)
-        cur_returns.extend(episode_returns.cpu().tolist())
-        n_test_runs = max(1, getattr(self.args, "test_nepisode", B) // B) * B
+        # infos of terminated envs carry `_step_count` (marl_partial.py:310) and every env
+        # has terminated when the loop ends: their sum is the sum of the episode lengths
+        total_len = int(lengths.sum())
+        cur_stats["_step_count"] = total_len + cur_stats.get("_step_count", 0)
+        cur_stats["n_episodes"] = self.batch_size + cur_stats.get("n_episodes", 0)
+        cur_stats["ep_length"] = total_len + cur_stats.get("ep_length", 0)
+        cur_returns.extend(returns)
+        n_test_runs = max(1, getattr(self.args, "test_nepisode", self.batch_size)
+                          // self.batch_size) * self.batch_size
         if test_mode and (len(self.test_returns) == n_test_runs):
             self._log(cur_returns, cur_stats, log_prefix)
-        elif self.t_env - self.log_train_stats_t >= getattr(self.args, "runner_log_interval", 1 << 62):
+        elif self.t_env - self.log_train_stats_t >= getattr(self.args, "runner_log_interval",
+                                                            1 << 62):
             self._log(cur_returns, cur_stats, log_prefix)
             sel = getattr(self.mac, "action_selector", None)
             if self.logger is not None and hasattr(sel, "epsilon"):

@@ -8,7 +8,7 @@ import numpy as np
 
 from conftest import REPO
 
-HEADERS = [os.path.join(REPO, "include", h) for h in ("mapfx.h", "mapfx_partial.h", "mapfx_primal.h")]
+HEADERS = [os.path.join(REPO, "include", h) for h in ("mapfx.h", "mapfx_partial.h", "mapfx_primal.h", "mapfx_runner.h")]
 
 
 def _declared():

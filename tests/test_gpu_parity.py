@@ -478,3 +478,47 @@ def test_overlapped_gather_single_rank(mapfx_mod):
                 assert torch.equal(got[i][k], ref[i][k]), (i, k)
     finally:
         dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------
+# 7. the drop-in step's host traffic: one packed D2H copy, one synchronisation
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("env_name", ["mapf_gridworld", "marl_partial"])
+def test_dropin_step_syncs_once(mapfx_mod, monkeypatch, env_name):
+    """A drop-in step waits on the device exactly once (the packed pull) and never
+    through an implicit sync (.item() / .cpu() / .tolist() / bool of a tensor)."""
+    import os
+    import random
+    from mapfx.envs import REGISTRY
+    scen = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "scen")
+    random.seed(1)   # draws empty-8-8-random-19.scen (kept in tests/golden/scen)
+    env = REGISTRY[env_name](grid_file_path=os.path.join(scen, "empty-8-8.map"),
+                             agents_path=os.path.join(scen, "empty-8-8-random-"), n_agents=4)
+    if env_name == "marl_partial":   # reset re-draws: pin the draw to a scen file that is present
+        env._MARL_PARTIAL_ENV__setup_agent = lambda: None
+    env.reset()
+    torch.cuda.synchronize()
+    calls = {"sync": 0}
+    real_sync = torch.cuda.Stream.synchronize
+
+    def counting_sync(self):
+        calls["sync"] += 1
+        return real_sync(self)
+
+    def guard(name):
+        real = getattr(torch.Tensor, name)
+
+        def f(self, *a, **k):
+            if self.is_cuda:
+                raise AssertionError("implicit device sync (%s) in a drop-in step" % name)
+            return real(self, *a, **k)
+        return f
+
+    monkeypatch.setattr(torch.cuda.Stream, "synchronize", counting_sync)
+    for name in ("item", "cpu", "tolist", "__bool__"):
+        monkeypatch.setattr(torch.Tensor, name, guard(name))
+    rs = np.random.RandomState(0)
+    for k in range(20):
+        env.step(rs.randint(0, 5, size=4).tolist())
+        assert calls["sync"] == k + 1
+    monkeypatch.undo()

@@ -1,122 +1,161 @@
 """GPU test of the batched ParallelRunner (mapfx/runners.py)
-against the reference runner's semantics (runners/parallel_runner.py:62-173)
-replayed on the CPU restatement of MARL_PARTIAL_ENV (oracle/partial_oracle.py):
-every EpisodeBatch field (state, obs, avail_actions, actions, reward, terminated,
-filled) equal, with some envs terminating early (completion) to exercise the
-runner's not-terminated bookkeeping."""
+against the REFERENCE runner: tests/golden/runner_*.npz were written by
+tests/golden/gen_runner_fixtures.py running MARL-curve-main/src/runners/
+parallel_runner.py (forked env workers, Pipe protocol) into the reference
+components/episode_buffer.py EpisodeBatch with PyMARL's scheme and OneHot actions
+preprocess, under the scripted MAC restated below.  Every transition field of
+every run (state, obs, avail_actions, actions, actions_onehot, reward,
+terminated, filled), t_env and the logged stats must be equal; the fixtures have
+envs that terminate early at different steps (the stale not-terminated list)."""
 import types
 
 import numpy as np
 import pytest
 import torch
 
-from mapfx.episode import DeviceEpisodeBatch
-
 pytestmark = pytest.mark.gpu
 
-YAML = dict(obs_window=5, obs_knn_agents=5, episode_limit=20, move_reward=0, stay_reward=-0.1,
-            stay_goal_reward=1, node_collide_reward=-2000, edge_collide_reward=-2000,
-            env_collide_reward=-2000, complete_reward=1000, complete_fac=1.5, gamma=0.99)
+REWARDS = dict(move_reward=0, stay_reward=-0.1, stay_goal_reward=1, node_collide_reward=-2000,
+               edge_collide_reward=-2000, env_collide_reward=-2000, complete_reward=1000,
+               complete_fac=1.5, gamma=0.99)
+CASES = ["runner_open5_n2", "runner_wall6_n3", "runner_solo4_n1"]
+
+
+def scripted_action(b, t, n, avail_row):
+    """= gen_runner_fixtures.scripted_action"""
+    a = (3 * b + 7 * t + 5 * n + (b * t) % 3) % 5
+    return a if avail_row[a] else 4
 
 
 class ScriptedMAC:
-    """select_actions(batch, t_ep, t_env, bs, test_mode) from a fixed table; envs with
-    index % 4 == 0 always stay (they start on their goals and complete at t = 1)."""
+    action_selector = types.SimpleNamespace()
 
-    def __init__(self, table):
-        self.table = table  # [T, B, N] int64 (device)
-        self.calls = []
+    def __init__(self):
+        self.bs_lens = []
 
     def init_hidden(self, batch_size):
         pass
 
-    def select_actions(self, batch, t_ep, t_env, bs, test_mode=False):
-        self.calls.append(list(bs))
-        return self.table[t_ep][torch.as_tensor(bs, dtype=torch.long, device=self.table.device)]
+    def select_actions(self, batch, t_ep, t_env, bs=slice(None), test_mode=False):
+        avail = batch["avail_actions"][:, t_ep]
+        idx = bs.tolist() if isinstance(bs, torch.Tensor) else list(range(avail.shape[0]))[bs]
+        av = avail.cpu().numpy()
+        n = av.shape[1]
+        out = [[scripted_action(b, t_ep, k, av[b, k]) for k in range(n)] for b in idx]
+        return torch.tensor(out, dtype=torch.long, device=avail.device).view(len(idx), n)
 
 
-def _instances(B, S, N, seed=5):
-    rng = np.random.default_rng(seed)
-    cells = [(r, c) for r in range(S) for c in range(S)]
-    out = []
-    for e in range(B):
-        pick = rng.choice(len(cells), size=2 * N, replace=False)
-        st = [cells[i] for i in pick[:N]]
-        gl = list(st) if e % 4 == 0 else [cells[i] for i in pick[N:]]
-        out.append((st, gl))
-    return out
+class Logger:
+    def __init__(self):
+        self.stats = []
+
+    def log_stat(self, k, v, t):
+        self.stats.append((k, float(v), int(t)))
 
 
-def _reference_run(inst, table, S, N, T1):
-    """The reference runner loop (:62-173) over the CPU restatement."""
-    from oracle.partial_oracle import PartialEnvState
-    B = len(inst)
-    grid = np.zeros((S, S), dtype=np.int8)
-    envs = [PartialEnvState(grid, s, g, **YAML) for s, g in inst]
-    D = envs[0].obs().shape[1]
-    buf = {"state": np.zeros((B, T1, 3), np.float32), "obs": np.zeros((B, T1, N, D), np.float32),
-           "avail_actions": np.zeros((B, T1, N, 5), np.int32),
-           "actions": np.zeros((B, T1, N, 1), np.int64), "reward": np.zeros((B, T1, 1), np.float32),
-           "terminated": np.zeros((B, T1, 1), np.uint8), "filled": np.zeros((B, T1, 1), np.int64)}
-    for e, env in enumerate(envs):
-        buf["state"][e, 0] = env.state()
-        buf["obs"][e, 0] = env.obs()
-        buf["avail_actions"][e, 0] = env.avail()
-        buf["filled"][e, 0] = 1
-    terminated = [False] * B
-    not_term = list(range(B))
-    t = 0
-    while True:
-        for b in not_term:
-            buf["actions"][b, t, :, 0] = table[t, b]
-        stepping = [b for b in not_term if not terminated[b]]
-        not_term = [b for b in range(B) if not terminated[b]]
-        if all(terminated):
-            break
-        for b in stepping:
-            r, term = envs[b].step(table[t, b])
-            buf["reward"][b, t, 0] = np.float32(r)
-            buf["terminated"][b, t, 0] = term
-            terminated[b] = term
-        t += 1
-        for b in not_term:
-            buf["state"][b, t] = envs[b].state()
-            buf["obs"][b, t] = envs[b].obs()
-            buf["avail_actions"][b, t] = envs[b].avail()
-            buf["filled"][b, t] = 1
-    return buf
-
-
-def test_runner_matches_reference_runner_semantics(tmp_path):
-    if not torch.cuda.is_available():
-        pytest.skip("no HIP device")
+@pytest.mark.parametrize("name", CASES)
+def test_runner_matches_reference_parallel_runner(tmp_path, name):
+    from conftest import load_fixture
+    from mapfx.episode import DeviceEpisodeBatch, OneHot
     from mapfx.runners import ParallelRunner
-    S, N, B = 8, 6, 16
-    mp = tmp_path / "e.map"
-    mp.write_text("type octile\nheight 8\nwidth 8\nmap\n" + "\n".join(["." * 8] * 8) + "\n")
-    inst = _instances(B, S, N)
-    args = types.SimpleNamespace(env="marl_partial", batch_size_run=B, device="cuda",
-                                 env_args=dict(grid_file_path=str(mp), agents_path=str(tmp_path / "x-"),
-                                               n_agents=N, **YAML),
-                                 episode_batch_cls=DeviceEpisodeBatch, test_nepisode=B,
-                                 runner_log_interval=10 ** 9)
-    runner = ParallelRunner(args, None, instance_fn=lambda e: inst[e])
+    fx = load_fixture(name)
+    rows = [str(r) for r in fx["map"]]
+    s = len(rows)
+    mp = tmp_path / "m.map"
+    mp.write_text("type octile\nheight %d\nwidth %d\nmap\n%s\n" % (s, s, "\n".join(rows)))
+    B, N, limit = int(fx["B"]), int(fx["n_agents"]), int(fx["limit"])
+    starts, goals = fx["inst_starts"], fx["inst_goals"]   # [episodes, N, 2], one per run
+
+    def instance_fn(ep):
+        i = ep % starts.shape[0]
+        return np.repeat(starts[i][None], B, 0), np.repeat(goals[i][None], B, 0)
+
+    args = types.SimpleNamespace(
+        env="marl_partial", batch_size_run=B, device="cuda",
+        env_args=dict(REWARDS, grid_file_path=str(mp), agents_path=str(tmp_path / "x-"),
+                      n_agents=N, obs_window=int(fx["obs_window"]),
+                      obs_knn_agents=int(fx["obs_knn_agents"]), episode_limit=limit),
+        episode_batch_cls=DeviceEpisodeBatch, test_nepisode=B, runner_log_interval=1)
+    logger = Logger()
+    runner = ParallelRunner(args, logger, instance_fn=instance_fn)
     info = runner.get_env_info()
-    T1 = info["episode_limit"] + 1
-    rng = np.random.default_rng(9)
-    table = rng.integers(0, 5, size=(T1, B, N))
-    table[:, ::4, :] = 4
-    scheme = {"state": {"vshape": info["state_shape"]}, "obs": {"vshape": info["obs_shape"], "group": "agents"},
+    scheme = {"state": {"vshape": info["state_shape"]},
+              "obs": {"vshape": info["obs_shape"], "group": "agents"},
               "actions": {"vshape": (1,), "group": "agents", "dtype": torch.long},
               "avail_actions": {"vshape": (info["n_actions"],), "group": "agents", "dtype": torch.int},
               "reward": {"vshape": (1,)}, "terminated": {"vshape": (1,), "dtype": torch.uint8}}
-    mac = ScriptedMAC(torch.as_tensor(table, device="cuda"))
-    runner.setup(scheme, {"agents": N}, None, mac)
-    batch = runner.run(test_mode=False)
-    ref = _reference_run(inst, table, S, N, T1)
-    for k in ("state", "obs", "avail_actions", "actions", "reward", "terminated", "filled"):
-        got = batch.data.transition_data[k].cpu().numpy()
-        assert np.array_equal(got, ref[k].astype(got.dtype)), k
-    assert runner.t_env == int(ref["filled"].sum() - B)
-    # envs 0, 4, 8, 12 complete at t = 1; the others run to the episode limit
-    assert mac.calls[1] == list(range(B)) and 0 not in mac.calls[2]
+    runner.setup(scheme, {"agents": N}, {"actions": ("actions_onehot", [OneHot(out_dim=5)])},
+                 ScriptedMAC())
+    for r in range(int(fx["runs"])):
+        batch = runner.run(test_mode=False)
+        for k, v in batch.data.transition_data.items():
+            ref = fx["run%d_%s" % (r, k)]
+            got = v.cpu().numpy()
+            assert got.shape == ref.shape and got.dtype == ref.dtype, (r, k)
+            assert np.array_equal(got.view(np.uint8), ref.view(np.uint8)), (r, k)
+        assert runner.t_env == int(fx["run%d_t_env" % r])
+    assert [k for k, _, _ in logger.stats] == fx["log_stats"].tolist()
+    assert [v for _, v, _ in logger.stats] == fx["log_values"].tolist()
+    assert [t for _, _, t in logger.stats] == fx["log_t"].tolist()
+
+
+def test_runner_step_needs_no_host_sync(tmp_path, monkeypatch):
+    """Inside run(), between reset and the end-of-run totals, nothing reads a device
+    value on the host (no .item() / .tolist() / .cpu() / bool(tensor)); the only
+    waits are on the pinned ring's events, two steps old."""
+    from mapfx.episode import DeviceEpisodeBatch, OneHot
+    from mapfx.maps import synthetic_instances
+    from mapfx.runners import ParallelRunner
+    S, N, B = 8, 6, 64
+    mp = tmp_path / "e.map"
+    mp.write_text("type octile\nheight 8\nwidth 8\nmap\n" + "\n".join(["." * 8] * 8) + "\n")
+    inst = synthetic_instances(B, S, S, N, p_obstacle=0.0, seed=4)
+    args = types.SimpleNamespace(
+        env="marl_partial", batch_size_run=B, device="cuda",
+        env_args=dict(REWARDS, grid_file_path=str(mp), agents_path=str(tmp_path / "x-"),
+                      n_agents=N, episode_limit=30),
+        episode_batch_cls=DeviceEpisodeBatch, test_nepisode=B, runner_log_interval=1 << 62)
+    runner = ParallelRunner(args, None, instance_fn=lambda ep: (inst["init_pos"], inst["goals"]))
+    info = runner.get_env_info()
+
+    class DeviceMAC:
+        def init_hidden(self, batch_size):
+            pass
+
+        def select_actions(self, batch, t_ep, t_env, bs, test_mode=False):
+            av = batch["avail_actions"][bs, t_ep].float()
+            return torch.argmax(av * torch.rand(av.shape, device=av.device), dim=-1)
+
+    scheme = {"state": {"vshape": 3}, "obs": {"vshape": info["obs_shape"], "group": "agents"},
+              "actions": {"vshape": (1,), "group": "agents", "dtype": torch.long},
+              "avail_actions": {"vshape": (5,), "group": "agents", "dtype": torch.int},
+              "reward": {"vshape": (1,)}, "terminated": {"vshape": (1,), "dtype": torch.uint8}}
+    runner.setup(scheme, {"agents": N}, {"actions": ("actions_onehot", [OneHot(out_dim=5)])},
+                 DeviceMAC())
+    runner.run()                       # warm: first batch, caches
+    state = {"on": False}
+    real = {n: getattr(torch.Tensor, n) for n in ("item", "tolist", "cpu", "__bool__")}
+    steps_ptr = runner._env_steps.data_ptr()
+
+    def make(n):
+        def f(self, *a, **k):
+            if n == "item" and self.data_ptr() == steps_ptr:
+                state["on"] = False    # the end-of-run totals: the loop is over
+            if state["on"] and self.is_cuda:
+                raise AssertionError("%s() of a device tensor inside the runner loop" % n)
+            return real[n](self, *a, **k)
+        return f
+
+    for n in real:
+        monkeypatch.setattr(torch.Tensor, n, make(n))
+    real_step = runner.env.step
+
+    def step(a):
+        state["on"] = True
+        return real_step(a)
+
+    monkeypatch.setattr(runner.env, "step", step)
+    t_env0 = runner.t_env
+    runner.run()
+    monkeypatch.undo()
+    assert 0 < runner.t_env - t_env0 <= B * 30

@@ -20,7 +20,8 @@
  * mapfx_last_error().  Not restated (out of scope): the `output`
  * mode's random collision repair (:262-275) and the visualisation hooks.
  *
- * Limits: N <= 64, H, W <= 64 (the BFS and the step keep one env in one wavefront).
+ * Limits: N <= 64 (the step keeps one env in one wavefront), H, W <= 256 (one env's
+ * LDS maps within the CU's 160 KB; maps wider than 64 take the multi-wave BFS).
  */
 #ifndef MAPFX_PARTIAL_H
 #define MAPFX_PARTIAL_H

@@ -142,6 +142,73 @@ __global__ void __launch_bounds__(64) partial_bfs_kernel(PGeo g, const uint8_t* 
   for (int i = r; i < g.hw; i += 64) out[i] = dist[i];
 }
 
+// Maps wider or taller than 64 (up to 256 x 256): one 256-thread workgroup per
+// (env, agent); thread r holds row r as four 64-bit masks, the frontier rows are
+// exchanged through LDS (double-buffered, one barrier per level), distances go
+// straight to the table in global memory (its cells were set to -1 first).
+constexpr int BIGW = 4;  // 64-bit words per row: W <= 256
+__global__ void __launch_bounds__(256) partial_bfs_big_kernel(PGeo g, const uint8_t* bits,
+                                                              const int32_t* goal, const uint8_t* mask,
+                                                              int16_t* gd) {
+  __shared__ uint64_t front[2][256][BIGW];
+  const int pair = blockIdx.x;  // env * N + agent
+  const int env = pair / g.N;
+  if (mask && !mask[env]) return;  // uniform per block
+  const int r = threadIdx.x;
+  const int H = g.H, W = g.W;
+  int16_t* out = gd + (long long)pair * g.hw;
+  uint64_t freem[BIGW], seen[BIGW], cur[BIGW];
+#pragma unroll
+  for (int k = 0; k < BIGW; ++k) freem[k] = seen[k] = cur[k] = 0;
+  if (r < H) {
+    const uint8_t* b = bits + (g.map_shared ? 0 : (long long)env * g.map_stride);
+    for (int c = 0; c < W; ++c) {
+      const int idx = r * W + c;
+      if (!((b[idx >> 3] >> (idx & 7)) & 1)) freem[c >> 6] |= 1ull << (c & 63);
+    }
+    for (int c = 0; c < W; ++c) out[r * W + c] = -1;
+  }
+  const int gr = goal[2 * pair], gc = goal[2 * pair + 1];
+  if (r == gr && ((freem[gc >> 6] >> (gc & 63)) & 1)) {
+    cur[gc >> 6] = 1ull << (gc & 63);
+    seen[gc >> 6] = cur[gc >> 6];
+    out[r * W + gc] = 0;
+  }
+#pragma unroll
+  for (int k = 0; k < BIGW; ++k) front[0][r][k] = cur[k];
+  __syncthreads();
+  int level = 0, buf = 0;
+  bool any = true;
+  while (any) {
+    ++level;
+    uint64_t nxt[BIGW];
+#pragma unroll
+    for (int k = 0; k < BIGW; ++k) {
+      // same row: cells c-1 / c+1 (carries across the 64-bit words)
+      const uint64_t lft = (cur[k] << 1) | (k > 0 ? cur[k - 1] >> 63 : 0ull);
+      const uint64_t rgt = (cur[k] >> 1) | (k + 1 < BIGW ? cur[k + 1] << 63 : 0ull);
+      const uint64_t up = r > 0 ? front[buf][r - 1][k] : 0ull;
+      const uint64_t dn = r + 1 < 256 ? front[buf][r + 1][k] : 0ull;
+      nxt[k] = (lft | rgt | up | dn) & freem[k] & ~seen[k];
+    }
+    if (r >= H) {
+#pragma unroll
+      for (int k = 0; k < BIGW; ++k) nxt[k] = 0;
+    }
+    bool mine = false;
+#pragma unroll
+    for (int k = 0; k < BIGW; ++k) {
+      seen[k] |= nxt[k];
+      cur[k] = nxt[k];
+      front[buf ^ 1][r][k] = nxt[k];
+      mine |= nxt[k] != 0;
+      for (uint64_t m = nxt[k]; m; m &= m - 1) out[r * W + 64 * k + __builtin_ctzll(m)] = (int16_t)level;
+    }
+    buf ^= 1;
+    any = __syncthreads_or(mine ? 1 : 0) != 0;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Step / observe / reset kernel (one launch = one env step or observation pass).
 // ---------------------------------------------------------------------------
@@ -600,8 +667,8 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   if (!cfg || !out) return perr(MAPFX_EINVAL, "NULL argument");
   *out = nullptr;
   const mapfx_partial_cfg& c = *cfg;
-  if (c.H < 1 || c.W < 1 || c.H > 64 || c.W > 64)
-    return perr(MAPFX_EINVAL, "MARL_PARTIAL path supports 1 <= H, W <= 64");
+  if (c.H < 1 || c.W < 1 || c.H > 256 || c.W > 256)
+    return perr(MAPFX_EINVAL, "MARL_PARTIAL path supports 1 <= H, W <= 256");
   if (c.n_agents < 1 || c.n_agents > 64) return perr(MAPFX_EINVAL, "n_agents must be in 1..64");
   if (c.n_envs < 0) return perr(MAPFX_EINVAL, "n_envs < 0");
   if (c.episode_limit < 1) return perr(MAPFX_EINVAL, "episode_limit must be >= 1");
@@ -649,11 +716,13 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.env_rew = c.env_collide_reward;
   const int per_env = 2 * g.map_env_bytes + g.bits_env_bytes + g.feat_env_bytes + 64 * 8 +
                       g.rew_env_bytes;
+  // envs per wave: as many as fit 64 KB of LDS; one env may take up to the CU's
+  // 160 KB (maps up to 256 x 256), with the dynamic-LDS limit raised below
   int EPW = 64 / L;
   while (EPW > 1 && EPW * per_env > 64 * 1024) --EPW;
-  if (EPW * per_env > 64 * 1024) {
+  if (EPW * per_env > 160 * 1024) {
     delete h;
-    return perr(MAPFX_EINVAL, "configuration needs more than 64 KB of LDS per env (N * obs dim)");
+    return perr(MAPFX_EINVAL, "one env needs more than 160 KB of LDS (map too large)");
   }
   g.EPW = EPW;
   int off = 0;
@@ -664,6 +733,19 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.off_pos = off; off += EPW * 64 * 8;
   g.off_rew = off; off += EPW * g.rew_env_bytes;
   g.lds = off;
+  if (g.lds > 64 * 1024) {
+    int rc0 = MAPFX_OK;
+    for (auto fn : {partial_kernel<5, 5, 16>, partial_kernel<5, 5, 8>, partial_kernel<5, 5, 32>,
+                    partial_kernel<3, 5, 16>, partial_kernel<7, 5, 16>, partial_kernel<0, 0, 0>,
+                    partial_kernel<1, 0, 0>, partial_kernel<3, 0, 0>, partial_kernel<5, 0, 0>,
+                    partial_kernel<7, 0, 0>, partial_kernel<9, 0, 0>})
+      if (!rc0) rc0 = check_hip(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds),
+                                "hipFuncSetAttribute(partial_kernel LDS)");
+    if (rc0) {
+      delete h;
+      return rc0;
+    }
+  }
   // LUTs from the host libm (math.sqrt, float ** int): correctly rounded references
   const int S = std::max(c.H, c.W);
   g.sq_max = 2 * (S - 1) * (S - 1);
@@ -711,8 +793,12 @@ int mapfx_partial_goal_dist(mapfx_partial_t* h, const mapfx_partial_state* st,
   if (rc) return rc;
   const PGeo& g = h->geo;
   if ((long long)g.E * g.N == 0) return MAPFX_OK;
-  hipLaunchKernelGGL(partial_bfs_kernel, dim3(g.E * g.N), dim3(64), 0, (hipStream_t)stream, g,
-                     st->map_bits, st->goal, env_mask, st->goal_dist);
+  if (g.H <= 64 && g.W <= 64)
+    hipLaunchKernelGGL(partial_bfs_kernel, dim3(g.E * g.N), dim3(64), 0, (hipStream_t)stream, g,
+                       st->map_bits, st->goal, env_mask, st->goal_dist);
+  else
+    hipLaunchKernelGGL(partial_bfs_big_kernel, dim3(g.E * g.N), dim3(256), 0, (hipStream_t)stream, g,
+                       st->map_bits, st->goal, env_mask, st->goal_dist);
   return check_hip(hipGetLastError(), "partial_bfs_kernel launch");
 }
 

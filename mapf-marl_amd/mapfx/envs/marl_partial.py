@@ -32,9 +32,7 @@ class MARL_PARTIAL_ENV(MultiAgentEnv):
                  env_collide_reward=-1, complete_reward=1000, complete_fac=1.5, debug=False,
                  visual=False, gamma=0.99, output=False, device=None):
         assert os.path.exists(grid_file_path)                                    # :54
-        if output:
-            raise NotImplementedError("output mode (random collision repair, :262-275) is not "
-                                      "part of the MI355X path")
+        self._output_mode = bool(output)   # :58 (collision repair after the step, :262-275)
         self._grid_file_path = grid_file_path
         self._agent_path = agents_path
         self._render_mode = render
@@ -136,6 +134,7 @@ class MARL_PARTIAL_ENV(MultiAgentEnv):
             agents_action = agents_action.detach().cpu().numpy()
         assert len(agents_action) == self._n_agents                              # :173
         assert all([action_i in ACTION_MEANING.keys() for action_i in agents_action])  # :174
+        old_pos = list(self._agent_positions)
         self._act_host.numpy()[0] = [int(a) for a in agents_action]
         self._act_dev.copy_(self._act_host, non_blocking=True)
         self._batch.step(self._act_dev)
@@ -144,7 +143,39 @@ class MARL_PARTIAL_ENV(MultiAgentEnv):
         R = float(h["reward"][0])
         self._step_count += 1
         self._terminated = bool(h["terminated"][0])
+        if self._output_mode:
+            self._repair(old_pos, list(agents_action))
         return R, self._terminated, {'_step_count': self._step_count}
+
+    # ------------------------------------------------- output mode (:262-275)
+    def _repair(self, old_pos, actions):
+        """Rewards, at-goal flags and collision totals stay those of the raw step;
+        positions are made collision free like the reference's solvers; the node /
+        edge vectors the observation reads are then those of the last check (all
+        zero)."""
+        new = list(self._agent_positions)
+        n_node, node_vec = _check_node(new)                                      # :236
+        n_edge, _, pairs = _check_edge(old_pos, new)                             # :238
+        if n_node == 0 and n_edge == 0:
+            return
+        occ_old = self._grid.astype(np.int64).copy()    # the PRE-step _full_obs (:279-280)
+        for p in old_pos:
+            occ_old[p] += 1
+        ctx = (self._grid.shape, occ_old, old_pos, actions)
+        if n_node > 0:                                                           # :263-268
+            while n_node > 0:
+                new = _solve_node(ctx, new, node_vec)
+                n_node, node_vec = _check_node(new)
+        if n_edge > 0:                                                           # :269-275
+            while n_edge > 0:
+                new = _solve_edge(ctx, new, pairs)
+                n_edge, _, _ = _check_edge(old_pos, new)
+        b = self._batch
+        b.pos[0].copy_(torch.tensor(new, dtype=torch.int32))
+        b.node[0].zero_()
+        b.edge[0].zero_()
+        b.observe()
+        self._pull()
 
     def get_obs(self):
         """:312-317 -- (N, 2W^2 + 13K), float32 values."""
@@ -192,3 +223,160 @@ class MARL_PARTIAL_ENV(MultiAgentEnv):
 
     def episode_done(self):
         return bool(self._host["done"][0].all())
+
+
+# ---------------------------------------------------------------------------
+# output-mode collision repair, host side as in the reference (marl_partial.py):
+# sequential, randomised (random.shuffle on the global stream), data-dependent.
+# ---------------------------------------------------------------------------
+def _check_node(pos):
+    """__check_node_collisions (:747-770): (count, 0/1 vector)."""
+    at = {}
+    for i, p in enumerate(pos):
+        at.setdefault(p, set()).add(i)
+    vec = [0] * len(pos)
+    count = 0
+    for agents in at.values():
+        if len(agents) > 1:
+            count += len(agents)
+            for i in agents:
+                vec[i] += 1
+    return count, vec
+
+
+def _check_edge(old, new):
+    """__check_edge_collisions (:823-857): (count, vector, set of sorted pairs)."""
+    vec = [0] * len(new)
+    count = 0
+    pairs = set()
+    for i, (io, inew) in enumerate(zip(old, new)):
+        if io == inew:
+            continue
+        for j, jo in enumerate(old):
+            if j != i and jo == inew and new[j] == io:
+                count += 1
+                vec[i] += 1
+                pairs.add(tuple(sorted([i, j])))
+    return count, vec, pairs
+
+
+_DELTA = {0: (-1, 0), 1: (1, 0), 2: (0, -1), 3: (0, 1)}
+
+
+def _free(ctx, p):
+    """__is_valid and not __is_cell_obstacle on the pre-step occupancy (:504-522)."""
+    (h, w), occ, _, _ = ctx
+    return 0 <= p[0] < h and 0 <= p[1] < w and occ[p] != -1
+
+
+def _agent_step(ctx, act, pos):
+    """__agent_step (:617-643) -> (next_pos, env collision)."""
+    if act == 4:
+        return pos, False
+    d = _DELTA[act]
+    nxt = (pos[0] + d[0], pos[1] + d[1])
+    return (nxt, False) if _free(ctx, nxt) else (pos, True)
+
+
+def _solve_node(ctx, new, node_vec):
+    """__solve_node_collisions (:645-712)."""
+    _, _, old, acts = ctx
+    n = len(new)
+    col = [i for i in range(n) if node_vec[i] > 0]
+    random.shuffle(col)
+    cnt = {}
+    for p in new:
+        cnt[p] = cnt.get(p, 0) + 1
+    for a in col:
+        a_pos = new[a]
+        if cnt[a_pos] <= 1:
+            continue
+        a_new = old[a]
+        if cnt.get(a_new, 0) <= 0:
+            cnt[a_pos] -= 1
+            new[a] = a_new
+            cnt[a_new] = cnt.get(a_new, 0) + 1
+            continue
+        these = [i for i in range(n) if old[a] == new[i]]
+        random.shuffle(these)
+        these_acts = [acts[i] for i in these]
+        a_act = acts[a]
+        solved = False
+        for act in these_acts:
+            if act == a_act:
+                continue
+            p, coll = _agent_step(ctx, act, old[a])
+            if not coll and cnt.get(p, 0) <= 0:
+                cnt[a_pos] -= 1
+                new[a] = p
+                cnt[p] = cnt.get(p, 0) + 1
+                solved = True
+                break
+        if solved:
+            continue
+        tries = [0, 1, 2, 3]
+        random.shuffle(tries)
+        o = old[a]
+        for act in tries:
+            d = _DELTA[act]
+            p = (o[0] + d[0], o[1] + d[1])
+            if act == a_act or not _free(ctx, p):
+                continue
+            if cnt.get(p, 0) <= 0:
+                cnt[o] -= 1   # the reference decrements the OLD cell here (:706)
+                new[a] = p
+                cnt[p] = cnt.get(p, 0) + 1
+                break
+    return new
+
+
+def _solve_edge(ctx, new, pairs):
+    """__solve_edge_collisions (:772-821)."""
+    _, _, old, acts = ctx
+    try_map = {0: [2, 3], 1: [3, 2], 2: [0, 1], 3: [1, 0]}
+    back = {0: 1, 1: 0, 2: 3, 3: 2}
+    pairs = list(pairs)
+    random.shuffle(pairs)
+    cnt = {}
+    for p in new:
+        cnt[p] = cnt.get(p, 0) + 1
+    for pair in pairs:
+        pair = list(pair)
+        random.shuffle(pair)
+        solved = False
+        for a in pair:
+            a_pos = new[a]
+            broke = False
+            o = old[a]
+            for act in try_map[acts[a]]:
+                d = _DELTA[act]
+                p = (o[0] + d[0], o[1] + d[1])
+                if not _free(ctx, p):
+                    continue
+                if cnt.get(p, 0) <= 0:
+                    cnt[a_pos] -= 1
+                    new[a] = p
+                    cnt[p] = cnt.get(p, 0) + 1
+                    broke = True
+                    break
+            if broke:
+                solved = True
+                break
+        if solved:
+            continue
+        for a in pair:
+            o = old[a]
+            d = _DELTA[back[acts[a]]]
+            p = (o[0] + d[0], o[1] + d[1])
+            if not _free(ctx, p):
+                continue
+            if cnt.get(p, 0) <= 0:
+                cnt[a_pos] -= 1   # a_pos as left by the loop above (:807)
+                new[a] = p
+                cnt[p] = cnt.get(p, 0) + 1
+                solved = True
+        if solved:
+            continue
+        for a in pair:
+            new[a] = old[a]
+    return new

@@ -36,6 +36,8 @@ def _mask5(avail):
 @pytest.mark.parametrize("name", partial_fixtures())
 def test_partial_matches_reference_goldens(mapfx_mod, name):
     fx = load_fixture(name)
+    if "meta_output" in fx and bool(fx["meta_output"]):
+        pytest.skip("output=True repairs positions on the host: test_partial_dropin_output_mode")
     kw = {k: fx["meta_" + k].item() for k in KW}
     b = mapfx_mod.MarlPartialBatch(fx["init_pos"][None], fx["goals"][None], grids=fx["grid"][None],
                                    **kw)
@@ -64,7 +66,10 @@ def test_partial_matches_reference_goldens(mapfx_mod, name):
 
 
 @pytest.mark.parametrize("S,N,E,K,win,T", [(16, 8, 64, 5, 5, 40), (32, 16, 32, 5, 5, 30),
-                                           (12, 5, 40, 8, 3, 25), (24, 30, 6, 5, 7, 20)])
+                                           (12, 5, 40, 8, 3, 25), (24, 30, 6, 5, 7, 20),
+                                           # past 64 x 64: the multi-wave BFS, > 64 KB LDS maps
+                                           (100, 8, 3, 5, 5, 15), (65, 64, 2, 5, 3, 12),
+                                           (194, 16, 2, 4, 7, 10), (256, 6, 1, 5, 5, 8)])
 def test_partial_batch_matches_oracle(mapfx_mod, S, N, E, K, win, T):
     """Batched random instances (one free component, distinct starts / goals)."""
     from oracle.partial_oracle import PartialEnvState
@@ -135,6 +140,70 @@ def test_partial_dropin_env(mapfx_mod, tmp_path):
         assert np.float64(r).view(np.uint64) == fx["reward"][t].view(np.uint64), t
         assert term == bool(fx["terminated"][t])
         assert info["_step_count"] == t + 1
+        assert np.array_equal(env.get_obs(), fx["obs"][t].astype(np.float32)), t
+        assert np.array_equal(env.get_state(), fx["state"][t].astype(np.int64)), t
+        assert env.get_avail_actions() == fx["avail"][t].astype(int).tolist(), t
+
+
+def test_partial_bench_shape_matches_oracle(mapfx_mod):
+    """The bench's marl_partial workload itself (bench.py --env marl_partial: yaml config,
+    empty 8x8, 15 agents, 4096 envs, synthetic starts / goals) for a few steps, every
+    env against the CPU restatement."""
+    from mapfx.maps import synthetic_instances
+    from oracle.partial_oracle import PartialEnvState
+    import bench
+    S, N, E, T = 8, 15, 4096, 3
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.0, seed=1)
+    grid = np.zeros((S, S), dtype=np.int8)
+    b = mapfx_mod.MarlPartialBatch(inst["init_pos"], inst["goals"], grids=grid[None],
+                                   **bench.PARTIAL_YAML)
+    refs = [PartialEnvState(grid, inst["init_pos"][e], inst["goals"][e], **bench.PARTIAL_YAML)
+            for e in range(E)]
+    b.reset()
+    rng = np.random.default_rng(5)
+    for t in range(T):
+        acts = rng.integers(0, 5, size=(E, N))
+        out = b.step(torch.from_numpy(acts).cuda())
+        rr = [r.step(acts[e]) for e, r in enumerate(refs)]
+        rew = np.array([x[0] for x in rr], dtype=np.float64)
+        assert np.array_equal(_np(out["reward"]).view(np.uint64), rew.view(np.uint64)), t
+        assert np.array_equal(_np(b.pos), np.array([r.pos for r in refs])), t
+        assert np.array_equal(_np(out["obs"]), np.stack([r.obs() for r in refs]).astype(np.float32)), t
+        assert np.array_equal(_np(out["avail"]), np.stack([_mask5(r.avail()) for r in refs])), t
+
+
+def test_partial_dropin_output_mode(mapfx_mod, tmp_path):
+    """MARL_PARTIAL_ENV(output=True) through the registry against the reference run
+    with output=True (mp_out8_n5): the drop-in draws the same instance with the same
+    `random` calls, steps on the GPU, repairs collisions on the host (the global
+    `random` stream, as the reference) and re-observes on the GPU."""
+    import random
+    from mapfx.envs import REGISTRY
+    fx = load_fixture("mp_out8_n5")
+    grid = fx["grid"]
+    s = grid.shape[0]
+    mp = tmp_path / "m.map"
+    mp.write_text("type octile\nheight %d\nwidth %d\nmap\n" % (s, s) +
+                  "\n".join("".join("." if v == 0 else "@" for v in row) for row in grid) + "\n")
+    st, gl = fx["scen_starts"], fx["scen_goals"]
+    rows = ["0\tm.map\t%d\t%d\t%d\t%d\t%d\t%d\t0" % (s, s, a[1], a[0], b[1], b[0])
+            for a, b in zip(st, gl)]
+    rows.append(rows[0])
+    for k in range(1, 26):
+        (tmp_path / ("m-random-%d.scen" % k)).write_text("version 1\n" + "\n".join(rows) + "\n")
+    kw = {k: fx["meta_" + k].item() for k in KW}
+    random.seed(int(fx["meta_py_seed"]))
+    env = REGISTRY["marl_partial"](grid_file_path=str(mp), agents_path=str(tmp_path / "m-random-"),
+                                   n_agents=int(fx["init_pos"].shape[0]), output=True, **kw)
+    random.seed(int(fx["meta_reset_seed"]))
+    obs = env.reset()
+    assert np.array_equal(obs, fx["obs0"].astype(np.float32))
+    for t in range(fx["actions"].shape[0]):
+        r, term, info = env.step(list(fx["actions"][t]))
+        assert np.float64(r).view(np.uint64) == fx["reward"][t].view(np.uint64), t
+        assert term == bool(fx["terminated"][t])
+        assert [env.agent_pos(i) for i in range(len(fx["pos"][t]))] == \
+            [tuple(p) for p in fx["pos"][t].tolist()], t
         assert np.array_equal(env.get_obs(), fx["obs"][t].astype(np.float32)), t
         assert np.array_equal(env.get_state(), fx["state"][t].astype(np.int64)), t
         assert env.get_avail_actions() == fx["avail"][t].astype(int).tolist(), t

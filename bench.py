@@ -226,38 +226,52 @@ def main():
     outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done",
             "traj_t")
 
-    def plan(k0, t):
+    def plan(k0, t, events=None):
         tr = traj if t == T else {k: v[:t] for k, v in traj.items()}
-        return b.rollout_plan(t, actions=acts[k0:k0 + t], traj=tr, outputs=outs, stream=stream)
+        return b.rollout_plan(t, actions=acts[k0:k0 + t], traj=tr, outputs=outs, stream=stream,
+                              events=events)
 
     # ---- warmup: whole launches of the timed shape (>= W env steps) ----
     for i in range(n_wu):
         plan(i * T, T)()
     torch.cuda.synchronize()
-    # every timed launch prepared up front: the timed region is ctypes calls only
+    # every timed launch prepared up front: the timed region is the ctypes calls only
+    # (no event packets in it: an event record costs ~3 us of wall time at this size,
+    # profiles/r02_wall_probe.json)
     k0 = n_wu * T
+    nl = n_full + (1 if rem else 0)
     plans = [plan(k0 + i * T, T) for i in range(n_full)]
     if rem:
         plans.append(plan(k0 + n_full * T, rem))
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)       # torch creates the HIP events at their first record():
-    e1.record(stream)       # do that here, not inside the timed region
+    # the kernel's launch duration, measured live right after the timed region on the
+    # same stream: the same launches again, each recording start / stop events at the
+    # kernel's own begin / end (hipExtLaunchKernel, mapfx_rollout_timed) -- the
+    # duration rocprofv3 reports for the kernel
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(nl)]
+    for a_, b_ in evs:      # torch creates the HIP events at their first record()
+        a_.record(stream)
+        b_.record(stream)
+    kplans = [plan(k0 + i * T, T, evs[i]) for i in range(n_full)]
+    if rem:
+        kplans.append(plan(k0 + n_full * T, rem, evs[-1]))
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
 
     # ---- timed: exactly K env steps of all envs ----
     t0 = time.perf_counter()
-    e0.record(stream)
     for pl in plans:
         pl()
-    e1.record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    kern_ms_total = e0.elapsed_time(e1)         # HIP events on the launch stream
+    for pl in kplans:       # kernel timing pass (untimed wall clock)
+        pl()
+    torch.cuda.synchronize()
+    kern_ms_total = sum(a_.elapsed_time(b_) for a_, b_ in evs)   # on the launch stream
     kern_ms = kern_ms_total / len(plans)
     el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if dist:
@@ -378,6 +392,9 @@ def main():
             "kernel_ms_per_launch": round(kern_ms, 5),
             "timing": {"wall_ms": round(elapsed * 1e3, 4),
                        "kernel_ms_events": round(kern_ms_total, 4),
+                       "kernel_timing": "per-launch start/stop events recorded at the "
+                                        "kernel's begin/end (hipExtLaunchKernel) on a replay "
+                                        "of the same launches right after the timed region",
                        "launches": len(plans),
                        "wall_over_kernel": round(elapsed * 1e3 / kern_ms_total, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

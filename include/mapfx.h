@@ -157,6 +157,14 @@ int mapfx_rollout(mapfx_t* h, const mapfx_state* st, int32_t T, const void* acti
                   int action_dtype, uint64_t seed, int32_t t0, int32_t autoreset,
                   const mapfx_out* traj, void* stream);
 
+/* mapfx_rollout with the launch's own start / stop timestamps recorded into
+ * `start_event` / `stop_event` (hipEvent_t, created by the caller) at the kernel's
+ * begin and end (hipExtLaunchKernel), i.e. the kernel duration rocprofv3 reports,
+ * without the event packets' dispatch gaps.  NULL events: plain mapfx_rollout. */
+int mapfx_rollout_timed(mapfx_t* h, const mapfx_state* st, int32_t T, const void* actions,
+                        int action_dtype, uint64_t seed, int32_t t0, int32_t autoreset,
+                        const mapfx_out* traj, void* start_event, void* stop_event, void* stream);
+
 /* Fill out[T][E][N] (int8) with the generator's actions for steps t0..t0+T-1. */
 int mapfx_gen_actions(mapfx_t* h, uint64_t seed, int32_t t0, int32_t T, int8_t* out,
                       void* stream);

@@ -23,6 +23,7 @@
 //   * window observations are staged in LDS and leave as 16-byte stores.
 //
 // No MFMA: the step is integer gather/scatter + a short fp64 fold; HBM-bound.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -1794,7 +1795,8 @@ KernelFn pick_wave_kernel(int win, bool roll, bool fullw, bool runner, int L, bo
   return nullptr;
 }
 
-int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream) {
+int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = nullptr,
+           hipEvent_t ev1 = nullptr) {
   const Geo& g = h->geo;
   if (g.E == 0) return MAPFX_OK;
   // wave-local fast path: N <= 64, no PRIMAL output, window 3/5/7 (or none)
@@ -1814,15 +1816,22 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream) {
     KernelFn fn = pick_wave_kernel(a.obs_window ? g.window : 0, roll, fullw, runner, g.L, split);
     if (fn) {
       const int blocks = (g.E + g.EPW - 1) / g.EPW;
-      hipLaunchKernelGGL(fn, dim3(blocks), dim3(split ? 64 * MAPFX_SPLIT_WAVES : 64),
-                         split ? split_lds : g.wv_lds, stream, g, a);
+      const dim3 bt(split ? 64 * MAPFX_SPLIT_WAVES : 64);
+      const unsigned ldsb = split ? split_lds : g.wv_lds;
+      if (ev0 || ev1)
+        hipExtLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, ev0, ev1, 0, g, a);
+      else
+        hipLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, g, a);
       return check_hip(hipGetLastError(), "mapf_wave_kernel launch");
     }
   }
   KernelFn fn = pick_kernel(h->cell_bytes, h->APL, roll);
   const int blocks = (g.E + g.EPB - 1) / g.EPB;
   const int lds = g.off_stage + g.EPB * g.stage_env_bytes;
-  hipLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, g, a);
+  if (ev0 || ev1)
+    hipExtLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, ev0, ev1, 0, g, a);
+  else
+    hipLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, g, a);
   return check_hip(hipGetLastError(), roll ? "mapf_rollout_kernel launch" : "mapf_step_kernel launch");
 }
 
@@ -2212,6 +2221,32 @@ int mapfx_rollout(mapfx_t* h, const mapfx_state* st, int32_t T, const void* acti
   a.do_step = 1;
   a.pow_lut = h->pow_lut;
   return launch(h, a, true, (hipStream_t)stream);
+}
+
+int mapfx_rollout_timed(mapfx_t* h, const mapfx_state* st, int32_t T, const void* actions,
+                        int action_dtype, uint64_t seed, int32_t t0, int32_t autoreset,
+                        const mapfx_out* traj, void* start_event, void* stop_event, void* stream) {
+  if (!h) return set_error(MAPFX_EINVAL, "NULL handle");
+  int rc = check_state(h, st, autoreset != 0);
+  if (rc) return rc;
+  if ((rc = check_out(h, traj))) return rc;
+  if (T < 1) return set_error(MAPFX_EINVAL, "T < 1");
+  if (actions && (action_dtype < MAPFX_I8 || action_dtype > MAPFX_I64))
+    return set_error(MAPFX_EINVAL, "bad action_dtype %d", action_dtype);
+  Args a;
+  memset(&a, 0, sizeof(a));
+  fill_state_args(a, st);
+  fill_out_args(a, traj);
+  a.actions = actions;
+  a.act_dtype = action_dtype;
+  a.use_rng = actions ? 0 : 1;
+  a.seed = seed;
+  a.t0 = t0;
+  a.T = T;
+  a.autoreset = autoreset ? 1 : 0;
+  a.do_step = 1;
+  a.pow_lut = h->pow_lut;
+  return launch(h, a, true, (hipStream_t)stream, (hipEvent_t)start_event, (hipEvent_t)stop_event);
 }
 
 int mapfx_gen_actions(mapfx_t* h, uint64_t seed, int32_t t0, int32_t T, int8_t* out,

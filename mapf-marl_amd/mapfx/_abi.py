@@ -87,7 +87,7 @@ class QOut(ctypes.Structure):
 # (checked by tests/test_abi_exports.py)
 EXPORTS = ("mapfx_abi_version", "mapfx_last_error", "mapfx_map_stride", "mapfx_obs_elem_size",
            "mapfx_create", "mapfx_destroy", "mapfx_query", "mapfx_reset", "mapfx_step",
-           "mapfx_observe", "mapfx_rollout", "mapfx_gen_actions", "mapfx_action",
+           "mapfx_observe", "mapfx_rollout", "mapfx_rollout_timed", "mapfx_gen_actions", "mapfx_action",
            "mapfx_partial_create", "mapfx_partial_destroy", "mapfx_partial_obs_dim",
            "mapfx_partial_goal_dist", "mapfx_partial_reset", "mapfx_partial_step",
            "mapfx_partial_observe", "mapfx_primal_create", "mapfx_primal_destroy",
@@ -130,6 +130,8 @@ def _load():
         "mapfx_observe": (c_i32, [c_vp, P(State), P(Out), c_vp]),
         "mapfx_rollout": (c_i32, [c_vp, P(State), c_i32, c_vp, c_i32, c_u64, c_i32, c_i32, P(Out),
                                   c_vp]),
+        "mapfx_rollout_timed": (c_i32, [c_vp, P(State), c_i32, c_vp, c_i32, c_u64, c_i32, c_i32,
+                                        P(Out), c_vp, c_vp, c_vp]),
         "mapfx_gen_actions": (c_i32, [c_vp, c_u64, c_i32, c_i32, c_vp, c_vp]),
         "mapfx_action": (c_i32, [c_u64, c_i64, c_i32, c_i32]),
         "mapfx_partial_create": (c_i32, [P(PCfg), P(c_vp)]),

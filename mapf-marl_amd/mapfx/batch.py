@@ -274,7 +274,7 @@ class MapfGridBatch:
         return traj
 
     def rollout_plan(self, T, actions=None, seed=0, t0=0, autoreset=False, traj=None,
-                     outputs=None, stream=None):
+                     outputs=None, stream=None, events=None):
         """A prepared `rollout` launch: every argument is converted once, so calling
         the returned plan is one ctypes call (no tensor checks, no struct building).
         The plan keeps `actions` / `traj` alive and launches on `stream` (default:
@@ -285,7 +285,8 @@ class MapfGridBatch:
         return RolloutPlan(self, int(T), actions, ap, adt, int(seed) & 0xFFFFFFFFFFFFFFFF,
                            int(t0), 1 if autoreset else 0, traj,
                            self._out_struct(traj, keys=None if outputs is None else tuple(outputs)),
-                           stream if stream is not None else torch.cuda.current_stream(self.device))
+                           stream if stream is not None else torch.cuda.current_stream(self.device),
+                           events)
 
     def gen_actions(self, T, seed, t0=0, out=None):
         if out is None:
@@ -338,12 +339,19 @@ class RolloutPlan:
 
     __slots__ = ("batch", "T", "actions", "traj", "_fn", "_args")
 
-    def __init__(self, batch, T, actions, ap, adt, seed, t0, autoreset, traj, out, stream):
+    def __init__(self, batch, T, actions, ap, adt, seed, t0, autoreset, traj, out, stream,
+                 events=None):
         self.batch, self.T, self.actions, self.traj = batch, T, actions, traj
-        self._fn = lib.mapfx_rollout
         # byref objects keep `out` and the state struct alive with the plan
-        self._args = (batch._h, ctypes.byref(batch._state), T, ap, adt, seed, t0, autoreset,
-                      ctypes.byref(out), stream.cuda_stream)
+        if events is None:
+            self._fn = lib.mapfx_rollout
+            self._args = (batch._h, ctypes.byref(batch._state), T, ap, adt, seed, t0, autoreset,
+                          ctypes.byref(out), stream.cuda_stream)
+        else:   # (start, stop) torch.cuda.Event, recorded at the kernel's own begin / end
+            self._fn = lib.mapfx_rollout_timed
+            self._args = (batch._h, ctypes.byref(batch._state), T, ap, adt, seed, t0, autoreset,
+                          ctypes.byref(out), events[0].cuda_event, events[1].cuda_event,
+                          stream.cuda_stream)
 
     def __call__(self):
         rc = self._fn(*self._args)

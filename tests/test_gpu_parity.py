@@ -522,3 +522,30 @@ def test_dropin_step_syncs_once(mapfx_mod, monkeypatch, env_name):
         env.step(rs.randint(0, 5, size=4).tolist())
         assert calls["sync"] == k + 1
     monkeypatch.undo()
+
+
+def test_rollout_timed_equals_rollout(mapfx_mod):
+    """mapfx_rollout_timed (the bench's timed launch, hipExtLaunchKernel with start /
+    stop events) writes exactly what mapfx_rollout writes, and its events time it."""
+    from mapfx.maps import synthetic_instances
+    E, S, N, T = 512, 32, 16, 20
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=8)
+    mk = lambda: mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"],
+                                         hw=(S, S), episode_limit=50, obs=("window",),
+                                         track_steps=False)
+    b1, b2 = mk(), mk()
+    b1.reset()
+    b2.reset()
+    acts = b1.gen_actions(T, seed=3)
+    outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done",
+            "traj_t")
+    t1 = b1.rollout(T, actions=acts, outputs=outs)
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    ev[0].record()
+    ev[1].record()
+    t2 = b2.rollout_plan(T, actions=acts, outputs=outs, events=ev)()
+    torch.cuda.synchronize()
+    for k in outs:
+        assert torch.equal(t1[k], t2[k]), k
+    assert torch.equal(b1.pos, b2.pos) and torch.equal(b1.t, b2.t)
+    assert ev[0].elapsed_time(ev[1]) > 0.0

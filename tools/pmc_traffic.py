@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 outputs of bench.py into profiles/.
 
-  python tools/pmc_traffic.py --trace DIR --fetch DIR --write DIR --out profiles/pmc_c2.json
-      [--kernel mapf_rollout_kernel] [--config c2 --T 64 --E 4096]
+  python tools/pmc_traffic.py --trace DIR --fetch DIR --write DIR [--lds DIR] --out profiles/pmc_c2.json
+      [--kernel mapf_rollout_kernel] [--config c2 --T 64 --E 4096] [--command "..."]
 
 * --trace: a `rocprofv3 --kernel-trace --stats --output-format csv` directory; the
   per-kernel stats CSV is copied and the kernel's average duration recorded.
@@ -73,13 +73,40 @@ def trace_stats(d, kernel, out_dir, tag):
                         "total_ns": float(_col(r, "TotalDurationNs", "Total_Duration_Ns"))})
     # per-dispatch durations from the kernel trace
     durs = []
-    for r in _rows(d, "*kernel_trace.csv"):
-        if kernel in _col(r, "Kernel_Name", "KernelName"):
-            durs.append(int(_col(r, "End_Timestamp")) - int(_col(r, "Start_Timestamp")))
+    rows = [r for r in _rows(d, "*kernel_trace.csv") if kernel in _col(r, "Kernel_Name", "KernelName")]
+    rows.sort(key=lambda r: int(_col(r, "Start_Timestamp")))
+    for r in rows:
+        durs.append(int(_col(r, "End_Timestamp")) - int(_col(r, "Start_Timestamp")))
     if durs:
         res["dispatches"] = len(durs)
         res["median_ns"] = statistics.median(durs)
+        res["dispatch_ns"] = durs   # in launch order
     return res
+
+
+LDS_COUNTERS = ("SQ_WAVES", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
+                "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES")
+
+
+def lds_summary(d, kernel):
+    """LDS counters of the kernel (one `rocprofv3 --pmc` pass of 8 SQ counters),
+    averaged over its full-size dispatches, with the derived ratios."""
+    out = {}
+    for c in LDS_COUNTERS:
+        v, n = pmc_values(d, kernel, c)
+        if v is not None:
+            out[c] = v
+            out["dispatches"] = n
+    if out.get("SQ_LDS_IDX_ACTIVE"):
+        out["bank_conflict_cycles_frac"] = out.get("SQ_LDS_BANK_CONFLICT", 0.0) / out["SQ_LDS_IDX_ACTIVE"]
+    if out.get("SQ_WAVES"):
+        out["lds_insts_per_wave"] = out.get("SQ_INSTS_LDS", 0.0) / out["SQ_WAVES"]
+    if out.get("SQ_WAVE_CYCLES"):
+        out["lds_issue_stall_frac_of_wave_cycles"] = out.get("SQ_WAIT_INST_LDS", 0.0) / out["SQ_WAVE_CYCLES"]
+        out["lds_active_frac_of_wave_cycles"] = out.get("SQ_ACTIVE_INST_LDS", 0.0) / out["SQ_WAVE_CYCLES"]
+    out["note"] = ("SQ_LDS_BANK_CONFLICT = extra LDS-array cycles from bank conflicts, "
+                   "SQ_LDS_IDX_ACTIVE = all LDS-array cycles (MI355X_MICROARCH.md LDS)")
+    return out
 
 
 def main():
@@ -93,10 +120,14 @@ def main():
     ap.add_argument("--T", type=int, default=64)
     ap.add_argument("--E", type=int, default=4096)
     ap.add_argument("--tag", default="r01_c2")
+    ap.add_argument("--lds", default=None)
+    ap.add_argument("--command", default=None)
     a = ap.parse_args()
     out_dir = os.path.dirname(os.path.abspath(a.out))
     os.makedirs(out_dir, exist_ok=True)
     res = {"config": a.config, "T": a.T, "E": a.E, "kernel": a.kernel}
+    if a.command:
+        res["command"] = a.command
     if a.trace:
         res["trace"] = trace_stats(a.trace, a.kernel, out_dir, a.tag)
     fetch = write = None
@@ -111,6 +142,8 @@ def main():
     if fetch is not None and write is not None:
         res["traffic_bytes_per_launch"] = int((2.0 * fetch + write) * 1024)
         res["traffic_note"] = "(2*FETCH_SIZE + WRITE_SIZE)*1024: gfx950 FETCH_SIZE halving corrected"
+    if a.lds:
+        res["lds"] = lds_summary(a.lds, a.kernel)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))

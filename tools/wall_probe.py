@@ -25,6 +25,10 @@ traj.pop("reward_f32")
 outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done", "traj_t")
 st = torch.cuda.current_stream()
 plan = b.rollout_plan(T, actions=acts, traj=traj, outputs=outs, stream=st)
+xev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+xev[0].record(st)
+xev[1].record(st)
+xplan = b.rollout_plan(T, actions=acts, traj=traj, outputs=outs, stream=st, events=xev)
 tiny = torch.zeros(1, device="cuda")
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for _ in range(5):
@@ -75,6 +79,7 @@ for idle in (0.0, 0.002):
         run("plan_streamsync" + sfx, lambda: (plan(), st.synchronize()), idle),
         run("ev_plan_sync" + sfx, ev_plan, idle),
         run("plan_x2_sync" + sfx, lambda: (plan(), plan(), torch.cuda.synchronize()), idle),
+        run("extplan_sync" + sfx, lambda: (xplan(), torch.cuda.synchronize()), idle),
         run("plan_spin" + sfx, lambda: (plan(), spin()), idle),
         run("ev_plan_spin" + sfx, ev_plan_spin, idle),
         run("tiny_spin" + sfx, lambda: (tiny.fill_(1.0), spin()), idle),
@@ -109,7 +114,11 @@ def busy(n):
     return f
 
 
-for n in (0, 1, 10, 100, 400):
+for n in (0, 10):
     res.append(("ev_plan_sync_after_%d_launches" % n, *timed_after(busy(n), ev_plan)))
-res.append(("ev_plan_sync_after_50ms_sleep", *timed_after(lambda: time.sleep(0.05), ev_plan, 10)))
+    res.append(("extplan_sync_after_%d_launches" % n, *timed_after(busy(n), lambda: (xplan(), torch.cuda.synchronize()))))
+    res.append(("plan_sync_after_%d_launches" % n, *timed_after(busy(n), lambda: (plan(), torch.cuda.synchronize()))))
+xplan()
+torch.cuda.synchronize()
+res.append(("extplan_kernel_us", round(xev[0].elapsed_time(xev[1]) * 1e3, 2), None))
 print(json.dumps({k: [m, mn] for k, m, mn in res}, indent=0))

@@ -215,16 +215,20 @@ def main():
     inst = synthetic_instances(E, S, S, N, p_obstacle=p or 0.0, seed=1, env_offset=offset,
                                shared_grid=warehouse_grid(S) if shared else None)
     limit = 2 ** 31 - 1
+    # N > 127: agent counts need int16 cells; the window leaves as ONE int16 occupancy
+    # plane (obs_window_occ: obstacle = -1, agents = max(v, 0)), 2 B per window cell,
+    # instead of two int16 planes (the 0/1 obstacle plane would pay 2 B per cell)
+    wkind = "window_occ" if N > 127 else "window"
+    wkey = "obs_" + wkind
     b = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
-                            episode_limit=limit, obs=("window",), window=W,
+                            episode_limit=limit, obs=(wkind,), window=W,
                             device="cuda:%d" % local, env_offset=offset, track_steps=False)
     b.reset()
     stream = torch.cuda.current_stream()
     acts = b.gen_actions(n_wu * T + K, seed=2)                 # inputs resident in HBM
     traj = b._alloc_out(T)
     traj.pop("reward_f32")
-    outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done",
-            "traj_t")
+    outs = ("reward", "term", "node", "edge", "avail", wkey, "traj_pos", "traj_done", "traj_t")
 
     def plan(k0, t, events=None):
         tr = traj if t == T else {k: v[:t] for k, v in traj.items()}
@@ -294,12 +298,12 @@ def main():
     per_step = None
     if args.per_step_steps > 0:
         b2 = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
-                                 episode_limit=limit, obs=("window",), window=W,
+                                 episode_limit=limit, obs=(wkind,), window=W,
                                  device="cuda:%d" % local, env_offset=offset, track_steps=False)
         b2.reset()
         ks = args.per_step_steps
         na = acts.shape[0]
-        pouts = ("reward", "term", "node", "edge", "avail", "obs_window")
+        pouts = ("reward", "term", "node", "edge", "avail", wkey)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -344,7 +348,7 @@ def main():
     # ---- RCCL gather of (obs, reward, done) to rank 0 (N > 1: on by default) ----
     gather = None
     if dist and not args.no_gather:
-        gather = time_gather(dist, b, acts, outs, T, n_wu * T, K, world, E, N)
+        gather = time_gather(dist, b, acts, outs, T, n_wu * T, K, world, E, N, wkey)
 
     # ---- CPU baseline: the oracle's C restatement on this host (rank 0, N=1) ----
     cpu = None
@@ -380,11 +384,13 @@ def main():
             "dtype": "int32+f64",
             "data": "synthetic (splitmix64 random maps p=%.2f, distinct free starts/goals, "
                     "uniform random actions in HBM)" % (p or 0.0),
-            "config": {"workload": "%s: %dx%d %s, %d agents, %d envs/GPU, window %dx%d obs, "
+            "config": {"workload": "%s: %dx%d %s, %d agents, %d envs/GPU, window %dx%d obs%s, "
                                    "fused rollout T=%d env-steps per launch (%d launch%s)"
                                    % (args.config, S, S, "square synthetic warehouse (shelf "
                                       "blocks, stands in for highway_layout_v19)" if shared
-                                      else "grid", N, E, W, W, T, len(plans),
+                                      else "grid", N, E, W, W,
+                                      " (one int16 occupancy plane per agent)"
+                                      if wkind == "window_occ" else "", T, len(plans),
                                       "" if len(plans) == 1 else "es"),
                        "envs_total": total_envs, "agents": N, "grid": [S, S], "chunk_T": T,
                        "parallelism": "env-shard x%d" % world},
@@ -412,13 +418,13 @@ def main():
         dist.destroy_process_group()
 
 
-def time_gather(dist, b, acts, outs, T, k0, K, world, E, N):
+def time_gather(dist, b, acts, outs, T, k0, K, world, E, N, wkey="obs_window"):
     """The same K env steps as rollout chunks of T, each chunk's (window obs,
     reward, done) packed in one buffer and gathered to rank 0 with ONE RCCL gather
     on a side stream, overlapped with the next chunk (mapfx.dist.OverlappedGather).
     Rank 0 orders a read of every chunk after its gather (stream wait, no sync)."""
     from mapfx.dist import OverlappedGather
-    og = OverlappedGather(b, T, keys=("obs_window", "reward", "traj_done"), outputs=outs)
+    og = OverlappedGather(b, T, keys=(wkey, "reward", "traj_done"), outputs=outs)
     og.step_chunk(actions=acts[:T])                  # warm the communicator
     og.result(0)
     torch.cuda.synchronize()

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MAPFX_ABI_VERSION 1
+#define MAPFX_ABI_VERSION 2
 
 /* error codes */
 #define MAPFX_OK 0
@@ -86,7 +86,8 @@ typedef struct mapfx_state {
 } mapfx_state;
 
 /* Caller-owned device outputs; any pointer may be NULL (not produced).
- * obs_full / obs_window are int8 when N <= 127, else int16 (see mapfx_obs_elem_size). */
+ * obs_full / obs_window / obs_window_occ are int8 when N <= 127, else int16 (see
+ * mapfx_obs_elem_size). */
 typedef struct mapfx_out {
   double* reward;        /* [E]  sum(rewards) as the reference folds it (fp64)  */
   float* reward_f32;     /* [E]  same value rounded to fp32                      */
@@ -103,6 +104,12 @@ typedef struct mapfx_out {
   int32_t* traj_t;       /* [E]       post-step env step counter                 */
   int32_t* err;          /* [1] 0, or 1 + env index of an env given an action
                             outside 0..4 (that env is left unchanged)            */
+  void* obs_window_occ;  /* [E][N][w][w] the same window as ONE plane of occupancy
+                            values occ = agents - obstacle (the reference's map
+                            value, marl_partial.py:323-342): obstacle plane =
+                            (occ == -1), agents plane = max(occ, 0).  Half the bytes
+                            of obs_window; for N > 127 (int16 cells) it keeps the
+                            0/1 obstacle plane from costing 2 B per cell.  (ABI 2) */
 } mapfx_out;
 
 typedef struct mapfx_t mapfx_t;

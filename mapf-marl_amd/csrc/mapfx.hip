@@ -89,8 +89,10 @@ struct Geo {
   uint32_t m_pitch24;      // ceil(2^24 / pitch): cell -> row with one v_mul_hi_u32_u24
   int wpr;
   // LDS regions (byte offsets from the dynamic LDS base)
-  int off_map, off_bits, off_oldc, off_newc, off_rc, off_goal, off_rew, off_flag, off_stage;
+  int off_map, off_bits, off_oldc, off_newc, off_rc, off_goal, off_rew, off_flag;
   int map_env_bytes, bits_env_bytes, stage_env_bytes;
+  int gen_lds;             // dynamic LDS of a generic-kernel block
+  uint64_t m_N, m_w, m_ww, m_wlen;  // fastdiv magics for the block-cooperative window writer
   int window, wlen;        // marl_partial window w, 2*w*w
   int psize;               // PRIMAL observation size s
   int obs_mode;
@@ -131,6 +133,7 @@ struct Args {
   uint8_t* avail;
   void* obs_full;
   void* obs_window;
+  void* obs_window_occ;
   uint8_t* obs_primal;
   double* primal_vec;
   int32_t* traj_pos;
@@ -204,10 +207,165 @@ __device__ inline void fill_map(const Geo& g, uint32_t* map32, const uint32_t* b
   }
 }
 
+// 32-bit LDS address of a pointer into dynamic shared memory
+__device__ __forceinline__ __attribute__((unused)) uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+#ifndef MAPFX_GABL
+#define MAPFX_GABL 0  // diagnostic builds only: generic-kernel parts skipped for timing
+#endif
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations,
+// not for its global stores (a __syncthreads() drains every outstanding store --
+// a full HBM write latency per barrier).  No value produced in global memory is
+// read back inside a launch, so the step loop's barriers need LDS ordering only.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
+// Window observations of a block's envs (marl_partial.py:323-342), written by the
+// whole block straight from the post-step LDS maps: the block's output region is
+// contiguous ([env0 .. env0 + nenv) x N records), so thread t produces 16-byte
+// chunks t, t + BT, ... of it -- every store is a coalesced dwordx4 and no record
+// is staged.  Value j of the region is record q = j / VL, element i = j % VL, with
+// VL = 2 w^2 (OCC = false: obstacle plane then agents plane, es bytes each) or w^2
+// (OCC = true: the occupancy value occ = count - obstacle of each window cell, the
+// reference's own map value, from which obstacle = (occ == -1), agents =
+// max(occ, 0)).  Out-of-bounds window cells are the border's "obstacle, 0 agents".
+// ---------------------------------------------------------------------------
+template <typename CellT, bool OCC>
+__device__ __forceinline__ int window_elem(uint32_t cv, int plane) {
+  using CT = CellTraits<CellT>;
+  const int occ = (int)(cv & CT::CNT) - ((cv & CT::OE) ? 1 : 0);
+  if (OCC) return occ;
+  return plane ? (occ > 0 ? occ : 0) : (occ == -1 ? 1 : 0);
+}
+
+template <typename CellT, bool OCC>
+__device__ void write_windows(const Geo& g, const unsigned char* lds, const int* newc_blk,
+                              unsigned char* dst, int nvals, int tid, int nt) {
+  constexpr int es = (int)sizeof(CellT);
+  constexpr int VPC = 16 / es;  // values per 16-byte chunk
+  constexpr uint32_t VMASK = es == 1 ? 0xFFu : 0xFFFFu;
+  const int w = g.window, h = w >> 1, ww = w * w;
+  const int VL = OCC ? ww : 2 * ww;
+  const uint64_t mVL = OCC ? g.m_ww : g.m_wlen;
+  const int pitch = g.pitch;
+  const int nchunks = (((uintptr_t)dst & 15) == 0) ? nvals / VPC : 0;
+  for (int ch = tid; ch < nchunks; ch += nt) {
+    const int v = ch * VPC;
+    int q = fastdiv(v, mVL);
+    int i = v - q * VL;
+    int pl = 0;
+    if (!OCC && i >= ww) {
+      pl = 1;
+      i -= ww;
+    }
+    int y = fastdiv(i, g.m_w);
+    int x = i - y * w;
+    int slot = fastdiv(q, g.m_N);
+    const CellT* mp = (const CellT*)(lds + g.off_map + slot * g.map_env_bytes);
+    int base = newc_blk[q] - h * pitch - h;
+    uint32_t pk[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < VPC; ++j) {
+      const uint32_t cv = mp[base + y * pitch + x];
+      pk[(j * es) >> 2] |= ((uint32_t)window_elem<CellT, OCC>(cv, pl) & VMASK) << ((j * es * 8) & 31);
+      if (j + 1 < VPC && ++x == w) {  // advance to value v + j + 1
+        x = 0;
+        if (++y == w) {
+          y = 0;
+          if (!OCC && pl == 0) {
+            pl = 1;
+          } else {
+            pl = 0;
+            ++q;
+            slot = fastdiv(q, g.m_N);
+            mp = (const CellT*)(lds + g.off_map + slot * g.map_env_bytes);
+            base = newc_blk[q] - h * pitch - h;
+          }
+        }
+      }
+    }
+    ((uint4*)dst)[ch] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+  }
+  // unaligned region or the tail: one value per thread and store
+  for (int v = nchunks * VPC + tid; v < nvals; v += nt) {
+    const int q = fastdiv(v, mVL);
+    int i = v - q * VL;
+    int pl = 0;
+    if (!OCC && i >= ww) {
+      pl = 1;
+      i -= ww;
+    }
+    const int y = fastdiv(i, g.m_w), x = i - y * w;
+    const int slot = fastdiv(q, g.m_N);
+    const CellT* mp = (const CellT*)(lds + g.off_map + slot * g.map_env_bytes);
+    const int e = window_elem<CellT, OCC>(mp[newc_blk[q] + (y - h) * pitch + x - h], pl);
+    if (es == 1)
+      dst[v] = (unsigned char)e;
+    else
+      ((int16_t*)dst)[v] = (int16_t)e;
+  }
+}
+
+// obs_window_occ of u16 cells (N > 127, e.g. BASELINE C5), odd window W <= 7: one
+// thread per window ROW of a record (segment (q, y) = W int16 at byte offset
+// 2 (q W^2 + y W) of the block's region).  A row is (W + 1) / 2 + 1 LDS dwords
+// realigned with v_alignbyte; occ = (cell & 0x7FFF) - (cell >> 15) for two cells at
+// a time without a borrow between the halves (offset binary); it leaves as
+// (W - 1) / 2 dwords + one u16, aligned either way.  Consecutive threads write
+// consecutive rows (10 bytes apart at W = 5), ~5x fewer VALU operations per value
+// than the per-value writer above.
+template <int W>
+__device__ void write_occ16_rows(const Geo& g, const unsigned char* lds, const int* newc_blk,
+                                 unsigned char* dst, int nseg, int tid, int nt) {
+  constexpr int NP = (W + 1) / 2;  // cell pairs per row (the last one half used)
+  constexpr int h = W / 2;
+  typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+  const int pitch = g.pitch;
+  const uint32_t lbase = lds_addr(lds + g.off_map);
+  for (int sg = tid; sg < nseg; sg += nt) {
+    const int q = fastdiv(sg, g.m_w);
+    const int y = sg - q * W;
+    const int slot = fastdiv(q, g.m_N);
+    const int e0 = newc_blk[q] + (y - h) * pitch - h;          // first cell of the row
+    const uint32_t A = lbase + (uint32_t)(slot * g.map_env_bytes) + 2u * (uint32_t)e0;
+    lds_cu32* src = (lds_cu32*)(uintptr_t)(A & ~3u);
+    uint32_t Wd[NP + 1];
+#pragma unroll
+    for (int j = 0; j <= NP; ++j) Wd[j] = src[j];
+    const uint32_t sh = A & 2u;
+    uint32_t P[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const uint32_t c = __builtin_amdgcn_alignbyte(Wd[j + 1], Wd[j], sh);
+      P[j] = (((c & 0x7FFF7FFFu) | 0x80008000u) - ((c >> 15) & 0x00010001u)) ^ 0x80008000u;
+    }
+    const uint32_t O = 2u * (uint32_t)(q * (W * W) + y * W);
+    if ((O & 2u) == 0) {
+#pragma unroll
+      for (int j = 0; j + 1 < NP; ++j) *(uint32_t*)(dst + O + 4 * j) = P[j];
+      *(uint16_t*)(dst + O + 4 * (NP - 1)) = (uint16_t)P[NP - 1];
+    } else {
+      *(uint16_t*)(dst + O) = (uint16_t)P[0];
+#pragma unroll
+      for (int j = 0; j + 1 < NP; ++j)
+        *(uint32_t*)(dst + O + 2 + 4 * j) = __builtin_amdgcn_alignbyte(P[j + 1], P[j], 2);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // The step kernel: T fused steps (T = 1 for mapfx_step; do_step = 0 observes).
+// FEAT: bit 0 PRIMAL outputs (obs_primal / primal_vec), bit 1 obs_full; the
+// window / avail / reward path alone (FEAT 0) keeps its register budget <= 128
+// VGPRs, i.e. 4 blocks of 256 threads per CU.
 // ---------------------------------------------------------------------------
-template <typename CellT, int APL, bool ROLL>
+constexpr int FEAT_PRIM = 1, FEAT_FULL = 2;
+template <typename CellT, int APL, bool ROLL, int FEAT>
 __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   using CT = CellTraits<CellT>;
   extern __shared__ __align__(16) unsigned char lds[];
@@ -226,9 +384,8 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   int* newc = (int*)(lds + g.off_newc) + slot * N;
   int* rcs = (int*)(lds + g.off_rc) + slot * N;
   int* gls = (int*)(lds + g.off_goal) + slot * N;
-  double* rew = (double*)(lds + g.off_rew) + slot * N;
+  double* rew = (double*)(lds + g.off_rew) + slot * N;  // aliases bitsL (used after the build)
   int* flag = (int*)(lds + g.off_flag) + slot * 8;  // [parity*4 + {alldone, bad}]
-  unsigned char* stage_blk = lds + g.off_stage;
 
   // ---- per-lane agent state (registers) ----
   int r[APL], c[APL], gr[APL], gc[APL], st[APL];
@@ -249,7 +406,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       gc[k] = q.y;
       dn[k] = a.done[i] != 0;
       if (a.steps) st[k] = a.steps[i];
-      gls[ag] = (q.x << 16) | (q.y & 0xFFFF);
+      if constexpr ((FEAT & FEAT_PRIM) != 0) gls[ag] = (q.x << 16) | (q.y & 0xFFFF);
     }
   }
   int tcur = env_ok ? a.t[env] : 0;
@@ -278,8 +435,26 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   const long long Elong = g.E;
 
   const int T = ROLL ? a.T : 1;
+  // actions are loaded one step ahead: step s + 1's load is issued before step s's
+  // stores, so waiting for it never waits for them (vmcnt counts both, in order)
+  const bool read_act = a.do_step && !a.use_rng;
+  int act_nx[APL];
+#pragma unroll
+  for (int k = 0; k < APL; ++k)
+    act_nx[k] = (has[k] && read_act)
+                    ? load_action(a.actions, a.act_dtype, (long long)env * N + lane + k * g.L) : 4;
   for (int s = 0; s < T; ++s) {
     int* fl = flag + (s & 1) * 4;
+    int act_in[APL];
+#pragma unroll
+    for (int k = 0; k < APL; ++k) act_in[k] = act_nx[k];
+    if (ROLL && read_act && s + 1 < T) {
+#pragma unroll
+      for (int k = 0; k < APL; ++k)
+        if (has[k])
+          act_nx[k] = load_action(a.actions, a.act_dtype,
+                                  ((long long)(s + 1) * Elong + env) * N + lane + k * g.L);
+    }
     // ================= P0: move decision on the PRE-step map =================
     int oc[APL], nc[APL], act[APL], pre[APL];
     bool moved[APL], envc[APL];
@@ -296,7 +471,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         if (a.use_rng)
           av = gen_action(a.seed, g.env_offset + env, a.t0 + s, ag);
         else
-          av = load_action(a.actions, a.act_dtype, ((long long)s * Elong + env) * N + ag);
+          av = act_in[k];
         if (av < 0 || av > 4) {
           atomicOr(&fl[1], 1);
           av = 4;
@@ -318,7 +493,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         newc[ag] = nc[k];
       }
     }
-    __syncthreads();  // B1: every pre-step map read is done
+    lds_barrier();  // B1: every pre-step map read is done
     // ================= P1: move the agent counts =================
     const bool skip = (fl[1] != 0) || !a.do_step;
 #pragma unroll
@@ -335,10 +510,10 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         r[k] += act_dr(act[k]);
         c[k] += act_dc(act[k]);
       }
-      rcs[ag] = (r[k] << 16) | (c[k] & 0xFFFF);
+      if constexpr ((FEAT & FEAT_PRIM) != 0) rcs[ag] = (r[k] << 16) | (c[k] & 0xFFFF);
     }
     if (a.do_step && !skip && env_ok) ++tcur;
-    __syncthreads();  // B2: post-step map complete
+    lds_barrier();  // B2: post-step map complete
     // ================= P2: collisions, rewards, avail, observations =================
     const long long slotE = ROLL ? (long long)s * Elong : 0;  // trajectory slot offset (envs)
     // edge collisions (:364-383): i moved into a cell that had pre-step occupants;
@@ -349,7 +524,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     int edgek[APL];
 #pragma unroll
     for (int k = 0; k < APL; ++k) edgek[k] = 0;
-    if (g.L >= 64 && a.do_step && !skip) {
+    if (g.L >= 64 && a.do_step && !skip && !(MAPFX_GABL & 8)) {
       const int l64 = tid & 63;
 #pragma unroll
       for (int k = 0; k < APL; ++k) {
@@ -392,7 +567,8 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       } else if (a.do_step) {
         rew[ag] = 0.0;
       }
-      if (!dn[k]) atomicAnd(&fl[0], 0);
+      if (!dn[k]) fl[0] = 0;  // every writer stores the same 0: no atomic needed
+      if (MAPFX_GABL & 4) continue;
       if (a.do_step) {
         if (a.node) a.node[ai] = (uint8_t)node;
         if (a.edge) a.edge[ai] = (uint8_t)(edge > 255 ? 255 : edge);
@@ -408,30 +584,79 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         m |= ((uint32_t)map[cc + 1] != CT::OE) ? 8u : 0u;
         a.avail[ai] = (uint8_t)m;
       }
-      if (a.obs_window) {  // marl_partial.py:323-342 -> LDS staging
-        const int w = g.window, h = w >> 1;
-        unsigned char* dst = stage_blk + (size_t)(slot * N + ag) * wlen * es;
-        const int base = nc[k] - h * g.pitch - h;
-        for (int y = 0; y < w; ++y) {
-          for (int x = 0; x < w; ++x) {
-            const uint32_t v = map[base + y * g.pitch + x];
-            const int cnt = (int)(v & CT::CNT);
-            const int ob = (v & CT::OE) ? 1 : 0;
-            const int occ = cnt - ob;
-            const int o0 = (occ == -1) ? 1 : 0;
-            const int o1 = occ > 0 ? occ : 0;
-            if (es == 1) {
-              dst[y * w + x] = (unsigned char)o0;
-              dst[w * w + y * w + x] = (unsigned char)o1;
-            } else {
-              ((int16_t*)dst)[y * w + x] = (int16_t)o0;
-              ((int16_t*)dst)[w * w + y * w + x] = (int16_t)o1;
+    }
+    // ---- the env's lane-0 tail: the fp64 fold of the rewards, term, t, next flags ----
+    auto lane0_tail = [&](bool alldone) {
+      if (!env_ok || lane != 0) return;
+      if (a.do_step) {
+        if (fl[1] && a.err) atomicCAS(a.err, 0, env + 1);
+        double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
+        if (!(MAPFX_GABL & 1)) {
+          // the adds are one dependent chain; a ring of 8 LDS reads stays in flight
+          // ahead of it (the read of reward j + 8 is issued when reward j is added)
+          int j = 0;
+          if (N >= 8) {
+            double ring[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ring[i] = rew[i];
+            const int n8 = N & ~7;
+#pragma nounroll
+            for (j = 0; j < n8 - 8; j += 8) {
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                R = R + ring[i];
+                ring[i] = rew[j + 8 + i];
+                __builtin_amdgcn_sched_barrier(0);  // keep each read where it is issued
+              }
             }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) R = R + ring[i];
+            j = n8;
           }
+          for (; j < N; ++j) R = R + rew[j];
         }
+        if (a.reward) a.reward[slotE + env] = R;
+        if (a.reward_f32) a.reward_f32[slotE + env] = (float)R;
+      }
+      if (a.term) a.term[slotE + env] = alldone ? 1 : 0;
+      if (a.traj_t) a.traj_t[slotE + env] = tcur;
+      int* nf = flag + ((s + 1) & 1) * 4;
+      nf[0] = 1;
+      nf[1] = 0;
+    };
+    // One env per block over four waves (N > 128): wave 0 runs the tail (the fold is
+    // one dependent chain of N adds) while waves 1-3 write the window records.
+    const bool ovl = g.L == 256 && (a.obs_window || a.obs_window_occ);
+    if (ovl) {
+      lds_barrier();  // B2b: rew[] and the alldone flag complete
+      if (tid < 64) lane0_tail(fl[0] != 0);
+    }
+    const int wt0 = ovl ? 64 : 0;  // first writer thread
+    if ((a.obs_window || a.obs_window_occ) && !(MAPFX_GABL & 2) && tid >= wt0) {  // :323-342
+      const int wtid = tid - wt0, wnt = g.BT - wt0;
+      const int nenv = min(g.EPB, g.E - env0);
+      const long long rec0 = (slotE + env0) * (long long)N;  // first record of the block
+      const int* newc_blk = (const int*)(lds + g.off_newc);
+      if (a.obs_window)
+        write_windows<CellT, false>(g, lds, newc_blk,
+                                    (unsigned char*)a.obs_window + rec0 * wlen * es,
+                                    nenv * N * wlen, wtid, wnt);
+      if (a.obs_window_occ) {
+        unsigned char* dst = (unsigned char*)a.obs_window_occ + rec0 * (wlen / 2) * es;
+        bool done_occ = false;
+        if constexpr (sizeof(CellT) == 2) {
+          const int nseg = nenv * N * g.window;
+          done_occ = true;
+          if (g.window == 5) write_occ16_rows<5>(g, lds, newc_blk, dst, nseg, wtid, wnt);
+          else if (g.window == 3) write_occ16_rows<3>(g, lds, newc_blk, dst, nseg, wtid, wnt);
+          else if (g.window == 7) write_occ16_rows<7>(g, lds, newc_blk, dst, nseg, wtid, wnt);
+          else done_occ = false;
+        }
+        if (!done_occ)
+          write_windows<CellT, true>(g, lds, newc_blk, dst, nenv * N * (wlen / 2), wtid, wnt);
       }
     }
-    if (a.obs_primal || a.primal_vec) {  // rcs[] (written in P1) is visible since B2
+    if ((FEAT & FEAT_PRIM) && (a.obs_primal || a.primal_vec)) {  // rcs[] (P1) visible since B2
 #pragma unroll
       for (int k = 0; k < APL; ++k) {
         if (!has[k]) continue;
@@ -483,7 +708,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         }
       }
     }
-    if (a.obs_full && env_ok) {  // :143-192: row-major occ = count - flag
+    if ((FEAT & FEAT_FULL) && a.obs_full && env_ok) {  // :143-192: row-major occ = count - flag
       const long long HW = (long long)g.H * g.W;
       unsigned char* outb = (unsigned char*)a.obs_full + (slotE + env) * HW * es;
       if (es == 1 && (g.W & 3) == 0) {
@@ -510,40 +735,10 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         }
       }
     }
-    __syncthreads();  // B3: rew[], flags and staging complete
+    lds_barrier();  // B3: rew[] and flags complete
     // ================= P3: fold, term, staging copy-out, autoreset =================
     const bool alldone = fl[0] != 0;
-    if (env_ok && lane == 0) {
-      if (a.do_step) {
-        if (fl[1] && a.err) atomicCAS(a.err, 0, env + 1);
-        double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
-        for (int j = 0; j < N; ++j) R = R + rew[j];
-        if (a.reward) a.reward[slotE + env] = R;
-        if (a.reward_f32) a.reward_f32[slotE + env] = (float)R;
-      }
-      if (a.term) a.term[slotE + env] = alldone ? 1 : 0;
-      if (a.traj_t) a.traj_t[slotE + env] = tcur;
-      int* nf = flag + ((s + 1) & 1) * 4;
-      nf[0] = 1;
-      nf[1] = 0;
-    }
-    if (a.obs_window) {
-      const int nenv = min(g.EPB, g.E - env0);
-      const long long bytes = (long long)nenv * N * wlen * es;
-      unsigned char* dst =
-          (unsigned char*)a.obs_window + ((slotE + env0) * (long long)N * wlen) * es;
-      if ((((uintptr_t)dst) & 15) == 0 && (bytes & 15) == 0) {
-        const uint4* s4 = (const uint4*)stage_blk;
-        uint4* d4 = (uint4*)dst;
-        for (long long i = tid; i < (bytes >> 4); i += g.BT) d4[i] = s4[i];
-      } else if ((((uintptr_t)dst) & 3) == 0 && (bytes & 3) == 0) {
-        const uint32_t* s4 = (const uint32_t*)stage_blk;
-        uint32_t* d4 = (uint32_t*)dst;
-        for (long long i = tid; i < (bytes >> 2); i += g.BT) d4[i] = s4[i];
-      } else {
-        for (long long i = tid; i < bytes; i += g.BT) dst[i] = stage_blk[i];
-      }
-    }
+    if (!ovl) lane0_tail(alldone);
     // optional autoreset of envs whose agents are all done
 #pragma unroll
     for (int k = 0; k < APL; ++k) {
@@ -563,7 +758,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       }
     }
     if (a.autoreset && alldone && a.do_step) tcur = 0;
-    if (ROLL && s + 1 < T) __syncthreads();  // B4: map / staging reuse by the next step
+    if (ROLL && s + 1 < T) lds_barrier();  // B4: map reuse by the next step
   }
 
   // ---- write back the env state ----
@@ -871,10 +1066,6 @@ __device__ __forceinline__ void write_record(const uint32_t (&R)[4 * WIN], void*
   st_off(base, off + (odd ? 0u : (uint32_t)(REC - 2)), (uint16_t)(odd ? w[0] : w[NW - 1]));
 }
 
-// 32-bit LDS address of a pointer into dynamic shared memory
-__device__ __forceinline__ __attribute__((unused)) uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
 
 // Stage one agent's 2*WIN*WIN-byte window record in LDS.  Records are 2-byte
 // aligned (2*WIN^2 = 2 mod 4 for odd WIN): a record at 2 mod 4 is written as one
@@ -1685,15 +1876,15 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
 }
 
 // One env step (mapfx_step) or an observation pass (mapfx_observe, do_step = 0).
-template <typename CellT, int APL>
+template <typename CellT, int APL, int FEAT>
 __global__ void __launch_bounds__(256) mapf_step_kernel(Geo g, Args a) {
-  step_body<CellT, APL, false>(g, a);
+  step_body<CellT, APL, false, FEAT>(g, a);
 }
 
 // T fused env steps (mapfx_rollout); state stays in LDS / registers between steps.
-template <typename CellT, int APL>
+template <typename CellT, int APL, int FEAT>
 __global__ void __launch_bounds__(256) mapf_rollout_kernel(Geo g, Args a) {
-  step_body<CellT, APL, true>(g, a);
+  step_body<CellT, APL, true, FEAT>(g, a);
 }
 
 __global__ void reset_kernel(int E, int N, int32_t* pos, const int32_t* init_pos, uint8_t* done,
@@ -1740,25 +1931,29 @@ namespace {
 
 using KernelFn = void (*)(Geo, Args);
 
-KernelFn pick_kernel(int cell_bytes, int apl, bool roll) {
+template <typename CellT, int FEAT>
+KernelFn pick_kernel_cf(int apl, bool roll) {
   if (roll) {
-    if (cell_bytes == 1) {
-      if (apl == 1) return mapf_rollout_kernel<uint8_t, 1>;
-      if (apl == 2) return mapf_rollout_kernel<uint8_t, 2>;
-      return mapf_rollout_kernel<uint8_t, 4>;
-    }
-    if (apl == 1) return mapf_rollout_kernel<uint16_t, 1>;
-    if (apl == 2) return mapf_rollout_kernel<uint16_t, 2>;
-    return mapf_rollout_kernel<uint16_t, 4>;
+    if (apl == 1) return mapf_rollout_kernel<CellT, 1, FEAT>;
+    if (apl == 2) return mapf_rollout_kernel<CellT, 2, FEAT>;
+    return mapf_rollout_kernel<CellT, 4, FEAT>;
   }
-  if (cell_bytes == 1) {
-    if (apl == 1) return mapf_step_kernel<uint8_t, 1>;
-    if (apl == 2) return mapf_step_kernel<uint8_t, 2>;
-    return mapf_step_kernel<uint8_t, 4>;
-  }
-  if (apl == 1) return mapf_step_kernel<uint16_t, 1>;
-  if (apl == 2) return mapf_step_kernel<uint16_t, 2>;
-  return mapf_step_kernel<uint16_t, 4>;
+  if (apl == 1) return mapf_step_kernel<CellT, 1, FEAT>;
+  if (apl == 2) return mapf_step_kernel<CellT, 2, FEAT>;
+  return mapf_step_kernel<CellT, 4, FEAT>;
+}
+
+// feat: 0 (window / avail / rewards), FEAT_FULL, or FEAT_FULL | FEAT_PRIM
+template <typename CellT>
+KernelFn pick_kernel_c(int apl, bool roll, int feat) {
+  if (feat & FEAT_PRIM) return pick_kernel_cf<CellT, FEAT_FULL | FEAT_PRIM>(apl, roll);
+  if (feat & FEAT_FULL) return pick_kernel_cf<CellT, FEAT_FULL>(apl, roll);
+  return pick_kernel_cf<CellT, 0>(apl, roll);
+}
+
+KernelFn pick_kernel(int cell_bytes, int apl, bool roll, int feat) {
+  return cell_bytes == 1 ? pick_kernel_c<uint8_t>(apl, roll, feat)
+                         : pick_kernel_c<uint16_t>(apl, roll, feat);
 }
 
 int check_hip(hipError_t e, const char* what) {
@@ -1803,7 +1998,7 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
   const long long slot_elems = (long long)(roll ? a.T : 1) * g.E * g.N;
   const bool fits32 = slot_elems * std::max(8, 2 * g.window * g.window) < (1ll << 31) &&
                       (long long)(roll ? a.T : 1) * g.E * g.H * g.W < (1ll << 31);
-  if (g.wave_ok && fits32 && !a.obs_primal && !a.primal_vec) {
+  if (g.wave_ok && fits32 && !a.obs_primal && !a.primal_vec && !a.obs_window_occ) {
     const bool fullw = g.N == g.L && g.E % g.EPW == 0;
     const bool runner = roll && a.reward && a.term && a.node && a.edge && a.avail &&
                         a.traj_pos && a.traj_done && a.traj_t && a.obs_window && !a.obs_full;
@@ -1825,9 +2020,10 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
       return check_hip(hipGetLastError(), "mapf_wave_kernel launch");
     }
   }
-  KernelFn fn = pick_kernel(h->cell_bytes, h->APL, roll);
+  const int feat = (a.obs_primal || a.primal_vec) ? (FEAT_FULL | FEAT_PRIM) : a.obs_full ? FEAT_FULL : 0;
+  KernelFn fn = pick_kernel(h->cell_bytes, h->APL, roll, feat);
   const int blocks = (g.E + g.EPB - 1) / g.EPB;
-  const int lds = g.off_stage + g.EPB * g.stage_env_bytes;
+  const int lds = g.gen_lds;
   if (ev0 || ev1)
     hipExtLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, ev0, ev1, 0, g, a);
   else
@@ -1855,6 +2051,7 @@ void fill_out_args(Args& a, const mapfx_out* o) {
   a.avail = o->avail;
   a.obs_full = o->obs_full;
   a.obs_window = o->obs_window;
+  a.obs_window_occ = o->obs_window_occ;
   a.obs_primal = o->obs_primal;
   a.primal_vec = o->primal_vec;
   a.traj_pos = o->traj_pos;
@@ -1876,7 +2073,7 @@ int check_out(const mapfx_t* h, const mapfx_out* o) {
   const int m = h->cfg.obs_mode;
   if (o->obs_full && !(m & MAPFX_OBS_FULL))
     return set_error(MAPFX_EINVAL, "obs_full requested but MAPFX_OBS_FULL not in cfg.obs_mode");
-  if (o->obs_window && !(m & MAPFX_OBS_WINDOW))
+  if ((o->obs_window || o->obs_window_occ) && !(m & MAPFX_OBS_WINDOW))
     return set_error(MAPFX_EINVAL, "obs_window requested but MAPFX_OBS_WINDOW not in cfg.obs_mode");
   if ((o->obs_primal || o->primal_vec) && !(m & MAPFX_OBS_PRIMAL))
     return set_error(MAPFX_EINVAL, "PRIMAL obs requested but MAPFX_OBS_PRIMAL not in cfg.obs_mode");
@@ -1963,8 +2160,13 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   }
   const int cpw = 4 / es;  // cells per u32 word
   const int pl = round_up(P, cpw);
-  const int pitch = round_up(pl + c.W + P, 8 / es);  // rows 8-byte aligned (ds_write_b64 builds)
+  // u8 maps (the wave kernels): rows 8-byte aligned for the ds_write_b64 builds, left
+  // and right pads apart.  u16 maps (generic kernel only): the right pad of row r is
+  // the left pad of row r + 1 (pitch - W >= pl >= P cells between two rows' interiors),
+  // plus a tail of pl + P cells after the last row.
+  const int pitch = es == 1 ? round_up(pl + c.W + P, 8 / es) : round_up(c.W + pl, cpw);
   const int rows = c.H + 2 * P;
+  const int tail = es == 1 ? 0 : pl + P;
 
   g.H = c.H;
   g.W = c.W;
@@ -1978,7 +2180,7 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   g.pitch = pitch;
   g.rows = rows;
   g.wpr = pitch / cpw;
-  g.map_words = rows * g.wpr;
+  g.map_words = (rows * pitch + tail + cpw - 1) / cpw;
   g.m_wpr = magic48(g.wpr);
   g.m_W = magic48(c.W);
   g.m_W4 = magic48(std::max(1, c.W / 4));
@@ -1996,21 +2198,25 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   g.limit = c.episode_limit;
   g.step_rew = c.step_reward;
   g.collide_rew = c.collide_reward;
-  g.stage_env_bytes = (c.obs_mode & MAPFX_OBS_WINDOW) ? N * g.wlen * es : 0;
+  g.stage_env_bytes = (c.obs_mode & MAPFX_OBS_WINDOW) ? N * g.wlen * es : 0;  // wave kernels' staging
+  g.m_N = magic48(N);
+  g.m_w = magic48(std::max(1, c.window));
+  g.m_ww = magic48(std::max(1, c.window * c.window));
+  g.m_wlen = magic48(std::max(1, g.wlen));
+  const bool prim_arrays = (c.obs_mode & MAPFX_OBS_PRIMAL) != 0;
 
   if ((int64_t)c.H * c.W >= (1ll << 31) / 8 || g.map_words >= (1 << 30)) {
     delete h;
     return set_error(MAPFX_EINVAL, "grid too large");
   }
 
+  // generic block: maps | oldc | newc | [rc | goal: PRIMAL only] | bits == rew | flags
   auto lds_for = [&](int epb) {
     int off = 0;
     off += epb * g.map_env_bytes;
-    off += epb * g.bits_env_bytes;
-    off += 4 * round_up(epb * N * 4, 16);  // oldc, newc, rc, goal
-    off += round_up(epb * N * 8, 16);      // rew
-    off += round_up(epb * 8 * 4, 16);      // flags
-    off += epb * g.stage_env_bytes;
+    off += (prim_arrays ? 4 : 2) * round_up(epb * N * 4, 16);
+    off += std::max(epb * g.bits_env_bytes, round_up(epb * N * 8, 16));
+    off += round_up(epb * 8 * 4, 16);
     return off;
   };
   int EPB = 256 / L;
@@ -2026,21 +2232,22 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   int off = 0;
   g.off_map = off;
   off += EPB * g.map_env_bytes;
-  g.off_bits = off;
-  off += EPB * g.bits_env_bytes;
   g.off_oldc = off;
   off += round_up(EPB * N * 4, 16);
   g.off_newc = off;
   off += round_up(EPB * N * 4, 16);
-  g.off_rc = off;
-  off += round_up(EPB * N * 4, 16);
-  g.off_goal = off;
-  off += round_up(EPB * N * 4, 16);
-  g.off_rew = off;
-  off += round_up(EPB * N * 8, 16);
+  g.off_rc = g.off_goal = -1;
+  if (prim_arrays) {
+    g.off_rc = off;
+    off += round_up(EPB * N * 4, 16);
+    g.off_goal = off;
+    off += round_up(EPB * N * 4, 16);
+  }
+  g.off_bits = g.off_rew = off;  // the bitmap is dead once the map is built
+  off += std::max(EPB * g.bits_env_bytes, round_up(EPB * N * 8, 16));
   g.off_flag = off;
   off += round_up(EPB * 8 * 4, 16);
-  g.off_stage = off;
+  g.gen_lds = off;
 
   // wave-local fast path layout (one wavefront = EPW envs)
   g.wave_ok = 0;
@@ -2074,12 +2281,14 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     g.wave_ok = (o <= 64 * 1024 && pitch < 256 && g.rows * pitch < 65536) ? 1 : 0;
   }
 
-  const int lds_total = g.off_stage + EPB * g.stage_env_bytes;
+  const int lds_total = g.gen_lds;
   if (lds_total > 64 * 1024) {
     hipError_t e = hipSuccess;
+    const int feats[3] = {0, FEAT_FULL, FEAT_FULL | FEAT_PRIM};
     for (int roll = 0; roll < 2 && e == hipSuccess; ++roll)
-      e = hipFuncSetAttribute((const void*)pick_kernel(es, h->APL, roll != 0),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_total);
+      for (int fi = 0; fi < 3 && e == hipSuccess; ++fi)
+        e = hipFuncSetAttribute((const void*)pick_kernel(es, h->APL, roll != 0, feats[fi]),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds_total);
     if (e != hipSuccess) {
       delete h;
       return set_error(MAPFX_EHIP, "hipFuncSetAttribute(LDS=%d): %s", lds_total,
@@ -2126,7 +2335,7 @@ int mapfx_query(const mapfx_t* h, mapfx_info* info) {
   info->agents_per_lane = (g.N + g.L - 1) / g.L;
   info->envs_per_block = g.EPB;
   info->block_threads = g.BT;
-  info->lds_bytes = g.off_stage + g.EPB * g.stage_env_bytes;
+  info->lds_bytes = g.gen_lds;
   info->cell_bytes = h->cell_bytes;
   info->pad = g.P;
   return MAPFX_OK;
@@ -2166,6 +2375,7 @@ int mapfx_observe(mapfx_t* h, const mapfx_state* st, const mapfx_out* out, void*
     a.avail = out->avail;
     a.obs_full = out->obs_full;
     a.obs_window = out->obs_window;
+    a.obs_window_occ = out->obs_window_occ;
     a.obs_primal = out->obs_primal;
     a.primal_vec = out->primal_vec;
   }

@@ -41,7 +41,7 @@ class Out(ctypes.Structure):
     _fields_ = [("reward", c_vp), ("reward_f32", c_vp), ("term", c_vp), ("node", c_vp),
                 ("edge", c_vp), ("avail", c_vp), ("obs_full", c_vp), ("obs_window", c_vp),
                 ("obs_primal", c_vp), ("primal_vec", c_vp), ("traj_pos", c_vp),
-                ("traj_done", c_vp), ("traj_t", c_vp), ("err", c_vp)]
+                ("traj_done", c_vp), ("traj_t", c_vp), ("err", c_vp), ("obs_window_occ", c_vp)]
 
 
 class Info(ctypes.Structure):
@@ -107,6 +107,9 @@ class RState(ctypes.Structure):  # include/mapfx_runner.h mapfx_runner_state
                             "env_steps", "env_actions")]
 
 
+ABI_VERSION = 2  # include/mapfx.h MAPFX_ABI_VERSION
+
+
 class MapfxError(RuntimeError):
     pass
 
@@ -156,6 +159,9 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.mapfx_abi_version() != ABI_VERSION:
+        raise ImportError("%s has ABI %d, the bindings expect %d: rebuild it"
+                          % (LIB_PATH, lib.mapfx_abi_version(), ABI_VERSION))
     return lib
 
 

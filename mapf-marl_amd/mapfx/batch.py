@@ -19,8 +19,9 @@ from ._abi import MAPFX_I8, MAPFX_I32, MAPFX_I64, MAPFX_OBS_FULL, MAPFX_OBS_PRIM
 from .maps import map_stride, pack_bits
 
 _DTYPES = {torch.int8: MAPFX_I8, torch.int32: MAPFX_I32, torch.int64: MAPFX_I64}
-OBS_MODES = {"full": MAPFX_OBS_FULL, "window": MAPFX_OBS_WINDOW, "primal": MAPFX_OBS_PRIMAL}
-_OBS_KEYS = ("term", "avail", "obs_full", "obs_window", "obs_primal", "primal_vec")
+OBS_MODES = {"full": MAPFX_OBS_FULL, "window": MAPFX_OBS_WINDOW, "window_occ": MAPFX_OBS_WINDOW,
+             "primal": MAPFX_OBS_PRIMAL}
+_OBS_KEYS = ("term", "avail", "obs_full", "obs_window", "obs_window_occ", "obs_primal", "primal_vec")
 
 
 def _stream_handle() -> int:
@@ -35,7 +36,9 @@ class MapfGridBatch:
     precomputed `bits` [E|1, map_stride]; `init_pos` / `goals` are [E, N, 2]
     (row, col).  `obs` selects which observation kinds are produced each step:
     "full" (get_obs/get_state occupancy), "window" (marl_partial window of
-    `window`), "primal" (PRIMAL _observe of `primal_size`).
+    `window`, [N, 2, w, w] obstacle / agents planes), "window_occ" (the same window
+    as one [N, w, w] plane of occupancy values: obstacle = (v == -1), agents =
+    max(v, 0); see window_planes), "primal" (PRIMAL _observe of `primal_size`).
     """
 
     def __init__(self, init_pos, goals, grids=None, bits=None, hw=None, episode_limit=10000,
@@ -147,6 +150,9 @@ class MapfGridBatch:
         if "window" in self.obs_kinds:
             w = self.window
             o["obs_window"] = (lead + (E, N, 2, w, w), self.obs_elem)
+        if "window_occ" in self.obs_kinds:
+            w = self.window
+            o["obs_window_occ"] = (lead + (E, N, w, w), self.obs_elem)
         if "primal" in self.obs_kinds:
             s = self.primal_size
             o["obs_primal"] = (lead + (E, N, 4, s, s), torch.uint8)
@@ -358,3 +364,9 @@ class RolloutPlan:
         if rc:
             check(rc, "mapfx_rollout")
         return self.traj
+
+
+def window_planes(occ):
+    """[..., w, w] occupancy window (obs_window_occ) -> [..., 2, w, w] {obstacle,
+    agents} planes, i.e. obs_window (envs/marl_partial.py:323-342)."""
+    return torch.stack(((occ == -1).to(occ.dtype), occ.clamp(min=0)), dim=-3)

@@ -138,6 +138,55 @@ def test_batched_step_matches_oracle(mapfx_mod, cfg):
         assert np.array_equal(_np(out["obs_window"]), ref["obs_window"]), (name, t)
 
 
+@pytest.mark.parametrize("cfg", CONFIGS, ids=[c[0] for c in CONFIGS])
+def test_window_occ_matches_oracle(mapfx_mod, cfg):
+    """obs_window_occ (one occupancy plane, generic kernel's block-cooperative writer)
+    decodes to the oracle's {obstacle, agents} window planes, every step."""
+    from mapfx.batch import window_planes
+    from oracle import corc
+    name, E, S, N, p, T, win, shared, limit = cfg
+    inst = _instances(mapfx_mod, E, S, N, p, shared)
+    init = inst["init_pos"].copy()
+    if name.startswith("dense"):
+        init = np.random.RandomState(1).randint(0, S, size=(E, N, 2)).astype(np.int32)
+    b = mapfx_mod.MapfGridBatch(init, inst["goals"], bits=inst["bits"], hw=(S, S),
+                                episode_limit=limit, obs=("window_occ",), window=win)
+    ob = corc.OracleBatch(inst["bits"], init, inst["goals"], S, S, limit=limit)
+    out = b.reset()
+    assert np.array_equal(_np(window_planes(out["obs_window_occ"])), ob.observe(window=win)["obs_window"])
+    rs = np.random.RandomState(7)
+    for t in range(min(T, 6)):
+        a = rs.randint(0, 5, size=(E, N)).astype(np.int8)
+        out = b.step(torch.from_numpy(a).cuda())
+        rstep = ob.step(a.astype(np.int32))
+        ref = ob.observe(window=win)
+        assert np.array_equal(_u64(_np(out["reward"])), _u64(rstep["reward"])), (name, t)
+        assert np.array_equal(_np(out["avail"]), ref["avail"]), (name, t)
+        assert np.array_equal(_np(window_planes(out["obs_window_occ"])), ref["obs_window"]), (name, t)
+
+
+def test_window_occ_full_stack(mapfx_mod):
+    """N = 256 agents stacked on one free cell: the occupancy value 256 needs the
+    int16 cells; both window formats carry it exactly."""
+    from mapfx.batch import window_planes
+    E, S, N = 3, 16, 256
+    init = np.full((E, N, 2), 7, dtype=np.int32)
+    goals = np.zeros((E, N, 2), dtype=np.int32)
+    grid = np.zeros((S, S), dtype=np.uint8)
+    grid[7, 9] = 1
+    b = mapfx_mod.MapfGridBatch(init, goals, grids=grid, episode_limit=100,
+                                obs=("window", "window_occ"), window=5)
+    out = b.reset()
+    occ = _np(out["obs_window_occ"])
+    assert occ.dtype == np.int16 and (occ[:, :, 2, 2] == 256).all()
+    assert (occ[:, :, 2, 4] == -1).all()                     # the obstacle at (7, 9)
+    assert np.array_equal(_np(window_planes(out["obs_window_occ"])), _np(out["obs_window"]))
+    out = b.step(torch.full((E, N), 4, dtype=torch.int8, device="cuda"))   # all stay
+    occ = _np(out["obs_window_occ"])
+    assert (occ[:, :, 2, 2] == 256).all()
+    assert np.array_equal(_np(window_planes(out["obs_window_occ"])), _np(out["obs_window"]))
+
+
 @pytest.mark.parametrize("S,N,s,E", [(32, 16, 10, 64), (64, 32, 10, 16), (20, 30, 7, 50),
                                      (128, 200, 11, 4)])
 def test_batched_primal_matches_oracle(mapfx_mod, S, N, s, E):
@@ -170,7 +219,10 @@ def test_batched_primal_matches_oracle(mapfx_mod, S, N, s, E):
     (8, 2, 300, 50, ("full", "window", "primal"), 5),
     (64, 64, 40, 8, ("full", "window"), 5),
     (64, 64, 40, 8, ("full", "window", "primal"), 5),
-    (128, 256, 4, 4, ("full", "window", "primal"), 5)])
+    (128, 256, 4, 4, ("full", "window", "primal"), 5),
+    (128, 256, 6, 6, ("window_occ",), 5),                  # C5 shape, the bench's outputs
+    (100, 300, 5, 5, ("window", "window_occ"), 7),          # APL 2
+    (32, 16, 300, 12, ("window_occ",), 3)])                 # u8 cells, 16 envs per block
 def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T, obs, win):
     from mapfx import rng
     from mapfx.maps import synthetic_instances
@@ -192,7 +244,7 @@ def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T, obs, win):
     for k in range(T):
         out = b3.step(acts[k])
         for key in ("reward", "node", "edge", "avail", "term", "obs_full", "obs_window",
-                    "obs_primal", "primal_vec"):
+                    "obs_window_occ", "obs_primal", "primal_vec"):
             if key not in out:
                 continue
             x = _np(out[key])
@@ -280,9 +332,11 @@ def test_rollout_matches_oracle_full_size(mapfx_mod, name, E, S, N, T, shared):
     """BASELINE C3 and C5 at their full env counts: a fused
     generator-action rollout equals the C oracle's, every env, bit for bit."""
     from oracle import corc
+    from mapfx.batch import window_planes
     inst = _instances(mapfx_mod, E, S, N, 0.10, shared, seed=1)
+    wkind = "window_occ" if N > 127 else "window"     # what bench.py emits for the config
     b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
-                                episode_limit=2000, obs=("window",))
+                                episode_limit=2000, obs=(wkind,))
     ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=2000)
     b.reset()
     traj = b.rollout(T, seed=2, t0=0)
@@ -294,12 +348,13 @@ def test_rollout_matches_oracle_full_size(mapfx_mod, name, E, S, N, T, shared):
     assert np.array_equal(_np(traj["node"][-1]), ref["node"]), name
     assert np.array_equal(_np(traj["edge"][-1]), ref["edge"]), name
     assert np.array_equal(_np(traj["avail"][-1]), ref["avail"]), name
-    assert np.array_equal(_np(traj["obs_window"][-1]), ref["obs_window"]), name
+    win = traj["obs_window"][-1] if wkind == "window" else window_planes(traj["obs_window_occ"][-1])
+    assert np.array_equal(_np(win), ref["obs_window"]), name
     # size-independent: every agent stays in bounds and the window's agent plane
     # counts each agent's own cell (>= 1)
     pos = _np(b.pos)
     assert pos.min() >= 0 and pos.max() < S
-    assert (_np(traj["obs_window"][-1])[:, :, 1, 2, 2] >= 1).all()
+    assert (_np(win)[:, :, 1, 2, 2] >= 1).all()
 
 
 def test_autoreset(mapfx_mod):

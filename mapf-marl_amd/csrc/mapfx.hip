@@ -143,6 +143,17 @@ struct Args {
   const double* pow_lut;
 };
 
+// The pointers a launch reads first also travel as leading scalar kernel parameters:
+// built with -amdgpu-kernarg-preload-count=16 they arrive in SGPRs (kernarg preload;
+// aggregates are never preloaded), so the state loads issue before the rest of the
+// kernargs has been fetched from memory.
+#define MAPFX_HOT_PARAMS                                                                     \
+  int32_t *hp_pos, const int32_t *hp_goal, uint8_t *hp_done, const uint8_t *hp_bits,       \
+      const void *hp_act, int32_t *hp_t
+#define MAPFX_HOT_APPLY(a) \
+  (a).pos = hp_pos, (a).goal = hp_goal, (a).done = hp_done, (a).bits = hp_bits, (a).actions = hp_act, (a).t = hp_t
+#define MAPFX_HOT_ARGS(a) (a).pos, (a).goal, (a).done, (a).bits, (a).actions, (a).t
+
 template <typename CellT>
 struct CellTraits;
 template <>
@@ -1338,7 +1349,9 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
 // so only A and D (a few dozen instructions) sit on the serial chain between
 // steps.  The last step's heavy part and tails run after the loop.
 template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false>
-__global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave_kernel(Geo g, Args a) {
+__global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g) {
+  Args a = a0;
+  MAPFX_HOT_APPLY(a);
   extern __shared__ __align__(16) unsigned char lds[];
   static_assert(!SPLIT || (ROLL && FULLW && RUNNER && LL == 16 && WIN > 0), "split: runner rollout, N = 16");
   if constexpr (SPLIT) {
@@ -1877,13 +1890,17 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
 
 // One env step (mapfx_step) or an observation pass (mapfx_observe, do_step = 0).
 template <typename CellT, int APL, int FEAT>
-__global__ void __launch_bounds__(256) mapf_step_kernel(Geo g, Args a) {
+__global__ void __launch_bounds__(256) mapf_step_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g) {
+  Args a = a0;
+  MAPFX_HOT_APPLY(a);
   step_body<CellT, APL, false, FEAT>(g, a);
 }
 
 // T fused env steps (mapfx_rollout); state stays in LDS / registers between steps.
 template <typename CellT, int APL, int FEAT>
-__global__ void __launch_bounds__(256) mapf_rollout_kernel(Geo g, Args a) {
+__global__ void __launch_bounds__(256) mapf_rollout_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g) {
+  Args a = a0;
+  MAPFX_HOT_APPLY(a);
   step_body<CellT, APL, true, FEAT>(g, a);
 }
 
@@ -1929,7 +1946,8 @@ struct mapfx_t {
 
 namespace {
 
-using KernelFn = void (*)(Geo, Args);
+using KernelFn = void (*)(int32_t*, const int32_t*, uint8_t*, const uint8_t*, const void*, int32_t*,
+                          Args, Geo);
 
 template <typename CellT, int FEAT>
 KernelFn pick_kernel_cf(int apl, bool roll) {
@@ -2014,9 +2032,9 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
       const dim3 bt(split ? 64 * MAPFX_SPLIT_WAVES : 64);
       const unsigned ldsb = split ? split_lds : g.wv_lds;
       if (ev0 || ev1)
-        hipExtLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, ev0, ev1, 0, g, a);
+        hipExtLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, ev0, ev1, 0, MAPFX_HOT_ARGS(a), a, g);
       else
-        hipLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, g, a);
+        hipLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, MAPFX_HOT_ARGS(a), a, g);
       return check_hip(hipGetLastError(), "mapf_wave_kernel launch");
     }
   }
@@ -2025,9 +2043,9 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
   const int blocks = (g.E + g.EPB - 1) / g.EPB;
   const int lds = g.gen_lds;
   if (ev0 || ev1)
-    hipExtLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, ev0, ev1, 0, g, a);
+    hipExtLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, ev0, ev1, 0, MAPFX_HOT_ARGS(a), a, g);
   else
-    hipLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, g, a);
+    hipLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, MAPFX_HOT_ARGS(a), a, g);
   return check_hip(hipGetLastError(), roll ? "mapf_rollout_kernel launch" : "mapf_step_kernel launch");
 }
 

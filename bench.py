@@ -251,14 +251,20 @@ def main():
     # same stream: the same launches again, each recording start / stop events at the
     # kernel's own begin / end (hipExtLaunchKernel, mapfx_rollout_timed) -- the
     # duration rocprofv3 reports for the kernel
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(nl)]
-    for a_, b_ in evs:      # torch creates the HIP events at their first record()
-        a_.record(stream)
-        b_.record(stream)
-    kplans = [plan(k0 + i * T, T, evs[i]) for i in range(n_full)]
-    if rem:
-        kplans.append(plan(k0 + n_full * T, rem, evs[-1]))
+    # (KREP passes of the K steps; the median pass is reported, so one disturbed launch
+    # does not move the roofline)
+    KREP = 5
+    evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for _ in range(nl)] for _ in range(KREP)]
+    for rep_evs in evs:     # torch creates the HIP events at their first record()
+        for a_, b_ in rep_evs:
+            a_.record(stream)
+            b_.record(stream)
+    kplans = []
+    for rep_evs in evs:
+        kplans += [plan(k0 + i * T, T, rep_evs[i]) for i in range(n_full)]
+        if rem:
+            kplans.append(plan(k0 + n_full * T, rem, rep_evs[-1]))
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -275,7 +281,8 @@ def main():
     for pl in kplans:       # kernel timing pass (untimed wall clock)
         pl()
     torch.cuda.synchronize()
-    kern_ms_total = sum(a_.elapsed_time(b_) for a_, b_ in evs)   # on the launch stream
+    kern_passes = sorted(sum(a_.elapsed_time(b_) for a_, b_ in rep_evs) for rep_evs in evs)
+    kern_ms_total = kern_passes[KREP // 2]     # median pass; events on the launch stream
     kern_ms = kern_ms_total / len(plans)
     el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if dist:
@@ -399,8 +406,10 @@ def main():
             "timing": {"wall_ms": round(elapsed * 1e3, 4),
                        "kernel_ms_events": round(kern_ms_total, 4),
                        "kernel_timing": "per-launch start/stop events recorded at the "
-                                        "kernel's begin/end (hipExtLaunchKernel) on a replay "
-                                        "of the same launches right after the timed region",
+                                        "kernel's begin/end (hipExtLaunchKernel) on %d replays "
+                                        "of the same launches right after the timed region; "
+                                        "median replay" % KREP,
+                       "kernel_ms_replays": [round(x, 4) for x in kern_passes],
                        "launches": len(plans),
                        "wall_over_kernel": round(elapsed * 1e3 / kern_ms_total, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -119,7 +119,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--T", type=int, default=64)
     ap.add_argument("--E", type=int, default=4096)
-    ap.add_argument("--tag", default="r01_c2")
+    ap.add_argument("--tag", required=True, help="stats CSV name: profiles/<tag>_kernel_stats.csv")
     ap.add_argument("--lds", default=None)
     ap.add_argument("--command", default=None)
     a = ap.parse_args()
@@ -130,6 +130,8 @@ def main():
         res["command"] = a.command
     if a.trace:
         res["trace"] = trace_stats(a.trace, a.kernel, out_dir, a.tag)
+        if not res["trace"].get("kernels"):
+            raise SystemExit("no kernel matching %r in %s" % (a.kernel, a.trace))
     fetch = write = None
     if a.fetch:
         fetch, nf = pmc_values(a.fetch, a.kernel, "FETCH_SIZE")

@@ -604,3 +604,35 @@ def test_rollout_timed_equals_rollout(mapfx_mod):
         assert torch.equal(t1[k], t2[k]), k
     assert torch.equal(b1.pos, b2.pos) and torch.equal(b1.t, b2.t)
     assert ev[0].elapsed_time(ev[1]) > 0.0
+
+
+@pytest.mark.parametrize("N,win", [(12, 5), (100, 3)])
+def test_nonsquare_highway_map(mapfx_mod, tmp_path, N, win):
+    """A non-square map in the highway generator's format (mapfx.highway, SURVEY
+    §8(f) F4) through the kernels (wave path at N = 12, generic at N = 100) and
+    the C oracle, step by step."""
+    from mapfx import highway as hw
+    from mapfx.maps import synthetic_instances
+    from oracle import corc
+    H, W = 13, 37
+    rows = ["".join("@" if (r % 4 in (1, 2) and c % 6 in (1, 2, 3, 4)) else "ewns"[(r + c) % 4]
+                    for c in range(W)) for r in range(H)]
+    hw.write_highway_outputs(str(tmp_path), rows, {}, {}, [], {"g_map": rows})
+    grid, _ = hw.read_highways(str(tmp_path / "highways.txt"))
+    E = 96
+    inst = synthetic_instances(E, H, W, N, seed=9, shared_grid=-grid.astype(np.int8))
+    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(H, W),
+                                episode_limit=40, obs=("full", "window"), window=win)
+    ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], H, W, limit=40)
+    b.reset()
+    rs = np.random.RandomState(3)
+    for t in range(20):
+        a = rs.randint(0, 5, size=(E, N)).astype(np.int8)
+        out = b.step(torch.from_numpy(a).cuda())
+        rstep = ob.step(a.astype(np.int32))
+        ref = ob.observe(window=win)
+        assert np.array_equal(_np(b.pos), ob.pos), t
+        assert np.array_equal(_u64(_np(out["reward"])), _u64(rstep["reward"])), t
+        assert np.array_equal(_np(out["avail"]), ref["avail"]), t
+        assert np.array_equal(_np(out["obs_full"]), ref["obs_full"]), t
+        assert np.array_equal(_np(out["obs_window"]), ref["obs_window"]), t

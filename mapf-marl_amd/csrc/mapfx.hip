@@ -2079,10 +2079,11 @@ void fill_out_args(Args& a, const mapfx_out* o) {
 }
 
 int check_state(const mapfx_t* h, const mapfx_state* st, bool need_init) {
-  if (!st || !st->pos || !st->goal || !st->done || !st->t || !st->map_bits)
+  if (!st) return set_error(MAPFX_EINVAL, "state is NULL");
+  if (h->geo.E == 0) return MAPFX_OK;  // an empty shard: every call is a no-op (empty tensors: NULL)
+  if (!st->pos || !st->goal || !st->done || !st->t || !st->map_bits)
     return set_error(MAPFX_EINVAL, "state: pos/goal/done/t/map_bits must be non-NULL");
   if (need_init && !st->init_pos) return set_error(MAPFX_EINVAL, "state: init_pos is NULL");
-  (void)h;
   return MAPFX_OK;
 }
 
@@ -2281,9 +2282,11 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     o += EPW * g.map_env_bytes;
     g.wv_off_bits = o;
     o += g.wv_fast ? 0 : EPW * g.wv_bits_env_bytes;  // the fast build reads the bitmap from global
-    // rew rows: N doubles rounded up to 2 (16 B), +2 doubles so the 4 envs of a wave
-    // start on different banks
-    g.wv_rew_row = (N + 1) / 2 * 2 + ((((N + 1) / 2 * 2) % 16) == 0 ? 2 : 0);
+    // rew rows: one double per LANE of the env (every lane writes its slot, +0.0 past
+    // N, and the L = 16 fold reads all 16), rounded up to 2 (16 B), +2 doubles so the
+    // envs of a wave start on different banks
+    const int rew_base = std::max((N + 1) / 2 * 2, L);
+    g.wv_rew_row = rew_base + ((rew_base % 16) == 0 ? 2 : 0);
     g.wv_rew_buf = round_up(EPW * g.wv_rew_row * 8, 16);
     g.wv_off_rew = o;
     o += 2 * g.wv_rew_buf;
@@ -2409,7 +2412,7 @@ int mapfx_step(mapfx_t* h, const mapfx_state* st, const void* actions, int actio
   int rc = check_state(h, st, false);
   if (rc) return rc;
   if ((rc = check_out(h, out))) return rc;
-  if (!actions) return set_error(MAPFX_EINVAL, "NULL actions");
+  if (!actions && h->geo.E > 0) return set_error(MAPFX_EINVAL, "NULL actions");
   if (action_dtype < MAPFX_I8 || action_dtype > MAPFX_I64)
     return set_error(MAPFX_EINVAL, "bad action_dtype %d", action_dtype);
   Args a;
@@ -2479,10 +2482,11 @@ int mapfx_rollout_timed(mapfx_t* h, const mapfx_state* st, int32_t T, const void
 
 int mapfx_gen_actions(mapfx_t* h, uint64_t seed, int32_t t0, int32_t T, int8_t* out,
                       void* stream) {
-  if (!h || !out) return set_error(MAPFX_EINVAL, "NULL handle/out");
+  if (!h) return set_error(MAPFX_EINVAL, "NULL handle");
   if (T < 0) return set_error(MAPFX_EINVAL, "T < 0");
   const long long total = (long long)T * h->geo.E * h->geo.N;
   if (total == 0) return MAPFX_OK;
+  if (!out) return set_error(MAPFX_EINVAL, "NULL out");
   const int bt = 256;
   hipLaunchKernelGGL(gen_actions_kernel, dim3((unsigned)((total + bt - 1) / bt)), dim3(bt), 0,
                      (hipStream_t)stream, total, h->geo.E, h->geo.N, (long long)h->geo.env_offset,

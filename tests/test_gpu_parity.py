@@ -636,3 +636,78 @@ def test_nonsquare_highway_map(mapfx_mod, tmp_path, N, win):
         assert np.array_equal(_np(out["avail"]), ref["avail"]), t
         assert np.array_equal(_np(out["obs_full"]), ref["obs_full"]), t
         assert np.array_equal(_np(out["obs_window"]), ref["obs_window"]), t
+
+
+def test_edge_shapes(mapfx_mod):
+    """Edge shapes the reference admits: an empty shard (E = 0: every call a no-op),
+    a 1 x 1 map with one agent (nothing is ever available but stay), window 1, and
+    the ABI's maximum N = 1024 (generic kernel, 4 agents per lane) against the C oracle."""
+    from mapfx.maps import synthetic_instances
+    from oracle import corc
+    # E = 0
+    b0 = mapfx_mod.MapfGridBatch(np.zeros((0, 3, 2), np.int32), np.zeros((0, 3, 2), np.int32),
+                                 grids=np.zeros((4, 4), np.uint8), obs=("full", "window"))
+    b0.reset()
+    b0.step(torch.zeros((0, 3), dtype=torch.int8, device="cuda"))
+    tr = b0.rollout(3, seed=1)
+    assert tr["reward"].shape == (3, 0)
+    # 1 x 1 map, one agent, window 1
+    b1 = mapfx_mod.MapfGridBatch(np.zeros((2, 1, 2), np.int32), np.zeros((2, 1, 2), np.int32),
+                                 grids=np.zeros((1, 1), np.uint8), obs=("full", "window"), window=1,
+                                 episode_limit=5)
+    out = b1.reset()
+    assert _np(out["avail"]).tolist() == [[16], [16]]
+    assert _np(out["obs_window"]).reshape(2, 2).tolist() == [[0, 1], [0, 1]]
+    out = b1.step(torch.tensor([[0], [3]], dtype=torch.int8, device="cuda"))
+    assert _np(b1.pos).reshape(2, 2).tolist() == [[0, 0], [0, 0]]
+    assert _np(out["term"]).tolist() == [1, 1]          # the start is the goal
+    # N = 1024 on 64 x 64
+    E, S, N = 3, 64, 1024
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.05, seed=6)
+    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                                episode_limit=50, obs=("full", "window", "window_occ"), window=5)
+    assert b.info()["agents_per_lane"] == 4
+    ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=50)
+    b.reset()
+    rs = np.random.RandomState(4)
+    from mapfx.batch import window_planes
+    for t in range(5):
+        a = rs.randint(0, 5, size=(E, N)).astype(np.int8)
+        out = b.step(torch.from_numpy(a).cuda())
+        rstep = ob.step(a.astype(np.int32))
+        ref = ob.observe(window=5)
+        assert np.array_equal(_np(b.pos), ob.pos), t
+        assert np.array_equal(_u64(_np(out["reward"])), _u64(rstep["reward"])), t
+        assert np.array_equal(_np(out["edge"]), rstep["edge"]), t
+        assert np.array_equal(_np(out["obs_full"]), ref["obs_full"]), t
+        assert np.array_equal(_np(out["obs_window"]), ref["obs_window"]), t
+        assert np.array_equal(_np(window_planes(out["obs_window_occ"])), ref["obs_window"]), t
+
+
+@pytest.mark.parametrize("N", [3, 6, 9, 11, 12, 13, 14, 15, 17, 24, 33, 47])
+def test_wave_partial_lane_groups(mapfx_mod, N):
+    """N below its lane group L = pow2ceil(N) (lanes past N carry no agent): the
+    per-step kernel and the fused rollout against the C oracle, E not a multiple of
+    the envs per wave.  (N = 9..14 once folded the next env's rewards.)"""
+    from mapfx.maps import synthetic_instances
+    from oracle import corc
+    E, S, T = 51, 12, 8
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=N)
+    kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=30, obs=("window",), window=5)
+    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
+    ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=30)
+    b.reset()
+    acts = b.gen_actions(T, 7)
+    traj = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw).rollout(T, actions=acts)
+    for t in range(T):
+        a = _np(acts[t])
+        out = b.step(acts[t])
+        rstep = ob.step(a.astype(np.int32))
+        ref = ob.observe(window=5)
+        for got in (out, {k: v[t] for k, v in traj.items()}):
+            assert np.array_equal(_u64(_np(got["reward"])), _u64(rstep["reward"])), (N, t)
+            assert np.array_equal(_np(got["node"]), rstep["node"]), (N, t)
+            assert np.array_equal(_np(got["edge"]), rstep["edge"]), (N, t)
+            assert np.array_equal(_np(got["avail"]), ref["avail"]), (N, t)
+            assert np.array_equal(_np(got["obs_window"]), ref["obs_window"]), (N, t)
+        assert np.array_equal(_np(b.pos), ob.pos), (N, t)

@@ -265,15 +265,16 @@ def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T, obs, win):
         assert np.array_equal(_np(bb.steps), _np(b3.steps))
 
 
-@pytest.mark.parametrize("E,T,win,autoreset", [
-    (4096, 64, 5, False),   # the bench shape
-    (256, 1, 5, False), (256, 2, 5, False), (256, 3, 3, False), (252, 17, 7, False),
-    (64, 40, 5, True)])
-def test_runner_rollout_every_step(mapfx_mod, E, T, win, autoreset):
-    """N = 16 runner rollouts (every PyMARL output, no full map) take the store-wave
-    kernel: each step's outputs must equal one step launch's, step by step."""
+@pytest.mark.parametrize("E,T,win,autoreset,N", [
+    (4096, 64, 5, False, 16),   # the bench shape
+    (256, 1, 5, False, 16), (256, 2, 5, False, 16), (256, 3, 3, False, 16), (252, 17, 7, False, 16),
+    (64, 40, 5, True, 16),
+    (250, 12, 5, False, 12), (130, 9, 3, True, 7), (66, 10, 5, False, 40)])  # N < L: generic lanes
+def test_runner_rollout_every_step(mapfx_mod, E, T, win, autoreset, N):
+    """Runner rollouts (every PyMARL output, no full map; N = 16 takes the store-wave
+    kernel): each step's outputs must equal one step launch's, step by step."""
     from mapfx.maps import synthetic_instances
-    S, N = 32 if not autoreset else 8, 16
+    S = 32 if not autoreset else 8
     inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=12)
     kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=2000 if not autoreset else 9,
               obs=("window",), window=win)

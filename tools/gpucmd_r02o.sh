@@ -12,7 +12,7 @@ rc=$?
 tail -3 $OUT/tests.log
 [ $rc -eq 0 ] || exit $rc
 B="--config c5 --gpus 1 --cpu-seconds 0 --per-step-steps 0"
-for v in base gabl1 gabl2; do
+for v in base nofw; do
   if [ $v = base ]; then unset MAPFX_LIB; else export MAPFX_LIB=$PWD/mapf-marl_amd/mapfx/libmapfx_$v.so; fi
   echo "[$(date +%T)] $v"
   timeout -k 10 300 python3 bench.py $B --steps 20 --warmup 5 > $OUT/$v.json 2> $OUT/$v.err || exit $?

@@ -104,6 +104,7 @@ struct Geo {
   int wv_bits_env_bytes, wv_rew_buf, wv_stage_buf, wv_rew_row;  // rew / staging are double-buffered
   int wv_off_split, wv_split_buf;  // store-wave split: double-buffered per-step output image
   int wv_fast;                     // build_map_rows_fast applies (W <= 64, pitch % 8 == 0)
+  int nblk;                        // grid size of the launch (set in the kernel from its kernargs)
 };
 #ifndef MAPFX_FAST_WPR
 #define MAPFX_FAST_WPR 24  // words per padded row handled by build_map_rows_fast
@@ -149,10 +150,28 @@ struct Args {
 // kernargs has been fetched from memory.
 #define MAPFX_HOT_PARAMS                                                                     \
   int32_t *hp_pos, const int32_t *hp_goal, uint8_t *hp_done, const uint8_t *hp_bits,       \
-      const void *hp_act, int32_t *hp_t
-#define MAPFX_HOT_APPLY(a) \
-  (a).pos = hp_pos, (a).goal = hp_goal, (a).done = hp_done, (a).bits = hp_bits, (a).actions = hp_act, (a).t = hp_t
-#define MAPFX_HOT_ARGS(a) (a).pos, (a).goal, (a).done, (a).bits, (a).actions, (a).t
+      const void *hp_act, int32_t *hp_t, uint32_t hp_geo, uint32_t hp_nm
+// ... and what the first loads' addresses need: hp_geo = H | W << 13 | P << 26 |
+// wv_fast << 31 (the bitmap stride follows from H, W: mapfx_map_stride) and hp_nm =
+// grid size | act_dtype << 27 | do_step << 29 | use_rng << 30 | map_shared << 31 (the
+// XCD-aware block order needs the grid size; gridDim comes from the implicit
+// kernargs).  14 dwords: all that kernel-argument preload fills next to the kernarg
+// pointer.
+#define MAPFX_HOT_APPLY(a, g)                                                                \
+  (a).pos = hp_pos, (a).goal = hp_goal, (a).done = hp_done, (a).bits = hp_bits,             \
+  (a).actions = hp_act, (a).t = hp_t,                                                       \
+  (g).H = (int)(hp_geo & 0x1FFFu), (g).W = (int)((hp_geo >> 13) & 0x1FFFu),                 \
+  (g).P = (int)((hp_geo >> 26) & 0x1Fu), (g).wv_fast = (int)(hp_geo >> 31),                \
+  (g).bits_words = ((g).H * (g).W + 31) >> 5, (g).map_shared = 0,                           \
+  (g).map_stride = (hp_nm >> 31) ? 0 : ((((g).H * (g).W + 7) >> 3) + 15) & ~15,            \
+  (g).nblk = (int)(hp_nm & 0x7FFFFFFu), (a).act_dtype = (int)((hp_nm >> 27) & 3u),         \
+  (a).do_step = (int)((hp_nm >> 29) & 1u), (a).use_rng = (int)((hp_nm >> 30) & 1u)
+#define MAPFX_HOT_ARGS(a, g, nb)                                                             \
+  (a).pos, (a).goal, (a).done, (a).bits, (a).actions, (a).t,                                \
+      (uint32_t)(g).H | ((uint32_t)(g).W << 13) | ((uint32_t)(g).P << 26) |                 \
+          ((uint32_t)(g).wv_fast << 31),                                                    \
+      (uint32_t)(nb) | ((uint32_t)((a).act_dtype & 3) << 27) | ((a).do_step ? 1u << 29 : 0u) | \
+          ((a).use_rng ? 1u << 30 : 0u) | ((g).map_shared ? 1u << 31 : 0u)
 
 template <typename CellT>
 struct CellTraits;
@@ -1349,14 +1368,15 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
 // so only A and D (a few dozen instructions) sit on the serial chain between
 // steps.  The last step's heavy part and tails run after the loop.
 template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false>
-__global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g) {
+__global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g0) {
   Args a = a0;
-  MAPFX_HOT_APPLY(a);
+  Geo g = g0;
+  MAPFX_HOT_APPLY(a, g);
   extern __shared__ __align__(16) unsigned char lds[];
   static_assert(!SPLIT || (ROLL && FULLW && RUNNER && LL == 16 && WIN > 0), "split: runner rollout, N = 16");
   if constexpr (SPLIT) {
     if (threadIdx.x >= 64) {  // the output side of the split
-      const int e0 = xcd_block(blockIdx.x, gridDim.x) * (64 / LL);
+      const int e0 = xcd_block(blockIdx.x, g.nblk) * (64 / LL);
       unsigned char* sp = lds + g.wv_off_split;
       unsigned char* own = sp + 2 * g.wv_split_buf;
       if (MAPFX_SPLIT_WAVES == 2) split_store_wave<WIN, LL, ROLE_ALL>(g, a, sp, own, e0, threadIdx.x & 63);
@@ -1383,7 +1403,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   const int ag = lane64 & (L - 1);    // agent index
   const int base = slot << lshift;    // first lane of this env
   const int EPW = 64 >> lshift;
-  const int env0 = xcd_block(blockIdx.x, gridDim.x) * EPW;
+  const int env0 = xcd_block(blockIdx.x, g.nblk) * EPW;
   const int env = env0 + slot;
   const int N = FIXN ? LL : g.N;
   const bool env_ok = FULLW || env < g.E;
@@ -1411,17 +1431,17 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   constexpr int RPF = 4;
   uint32_t pfw[RPF][3];
   if (g.wv_fast) fast_row_prefetch<RPF>(g, bsrc, ag, L, pfw);
+  int tcur = env_ok ? a.t[env] : 0;  // (issued first: its pointer is preloaded)
   int cur = 0, gcell = -1, st = 0;  // padded cell of the agent / of its goal
   bool dn = false;
   if (has) {
     const int2 p = ((const int2*)a.pos)[oa];
     const int2 q = ((const int2*)a.goal)[oa];
+    dn = a.done[oa] != 0;
     cur = cell0 + p.x * pitch + p.y;
     gcell = cell0 + q.x * pitch + q.y;
-    dn = a.done[oa] != 0;
     if (a.steps) st = a.steps[oa];
   }
-  int tcur = env_ok ? a.t[env] : 0;
   PSTAMP(0);
   const int T = ROLL ? a.T : 1;
   // Actions are fetched for AB steps at a time: one VMEM wait per block instead of
@@ -1890,17 +1910,19 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
 
 // One env step (mapfx_step) or an observation pass (mapfx_observe, do_step = 0).
 template <typename CellT, int APL, int FEAT>
-__global__ void __launch_bounds__(256) mapf_step_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g) {
+__global__ void __launch_bounds__(256) mapf_step_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g0) {
   Args a = a0;
-  MAPFX_HOT_APPLY(a);
+  Geo g = g0;
+  MAPFX_HOT_APPLY(a, g);
   step_body<CellT, APL, false, FEAT>(g, a);
 }
 
 // T fused env steps (mapfx_rollout); state stays in LDS / registers between steps.
 template <typename CellT, int APL, int FEAT>
-__global__ void __launch_bounds__(256) mapf_rollout_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g) {
+__global__ void __launch_bounds__(256) mapf_rollout_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g0) {
   Args a = a0;
-  MAPFX_HOT_APPLY(a);
+  Geo g = g0;
+  MAPFX_HOT_APPLY(a, g);
   step_body<CellT, APL, true, FEAT>(g, a);
 }
 
@@ -1947,7 +1969,7 @@ struct mapfx_t {
 namespace {
 
 using KernelFn = void (*)(int32_t*, const int32_t*, uint8_t*, const uint8_t*, const void*, int32_t*,
-                          Args, Geo);
+                          uint32_t, uint32_t, Args, Geo);
 
 template <typename CellT, int FEAT>
 KernelFn pick_kernel_cf(int apl, bool roll) {
@@ -2032,9 +2054,9 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
       const dim3 bt(split ? 64 * MAPFX_SPLIT_WAVES : 64);
       const unsigned ldsb = split ? split_lds : g.wv_lds;
       if (ev0 || ev1)
-        hipExtLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, ev0, ev1, 0, MAPFX_HOT_ARGS(a), a, g);
+        hipExtLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, ev0, ev1, 0, MAPFX_HOT_ARGS(a, g, blocks), a, g);
       else
-        hipLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, MAPFX_HOT_ARGS(a), a, g);
+        hipLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, MAPFX_HOT_ARGS(a, g, blocks), a, g);
       return check_hip(hipGetLastError(), "mapf_wave_kernel launch");
     }
   }
@@ -2043,9 +2065,9 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
   const int blocks = (g.E + g.EPB - 1) / g.EPB;
   const int lds = g.gen_lds;
   if (ev0 || ev1)
-    hipExtLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, ev0, ev1, 0, MAPFX_HOT_ARGS(a), a, g);
+    hipExtLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, ev0, ev1, 0, MAPFX_HOT_ARGS(a, g, blocks), a, g);
   else
-    hipLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, MAPFX_HOT_ARGS(a), a, g);
+    hipLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, MAPFX_HOT_ARGS(a, g, blocks), a, g);
   return check_hip(hipGetLastError(), roll ? "mapf_rollout_kernel launch" : "mapf_step_kernel launch");
 }
 
@@ -2142,7 +2164,8 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     return set_error(MAPFX_EINVAL, "grid %dx%d out of range", c.H, c.W);
   if (c.n_agents < 1 || c.n_agents > 1024)
     return set_error(MAPFX_EINVAL, "n_agents %d not in 1..1024", c.n_agents);
-  if (c.n_envs < 0) return set_error(MAPFX_EINVAL, "n_envs < 0");
+  if (c.n_envs < 0 || c.n_envs >= (1 << 27))  // the grid size travels in 27 bits (MAPFX_HOT_ARGS)
+    return set_error(MAPFX_EINVAL, "n_envs %d not in 0..2^27-1", c.n_envs);
   if ((c.obs_mode & MAPFX_OBS_WINDOW) && (c.window < 1 || c.window > 63))
     return set_error(MAPFX_EINVAL, "window %d not in 1..63", c.window);
   if ((c.obs_mode & MAPFX_OBS_PRIMAL) && (c.primal_size < 1 || c.primal_size > 11))

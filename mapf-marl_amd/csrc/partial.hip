@@ -45,7 +45,7 @@ struct PGeo {
   int bits_words, map_shared;
   long long map_stride;
   int map_env_bytes, bits_env_bytes, feat_env_bytes, rew_env_bytes;
-  int off_map, off_dep, off_bits, off_feat, off_pos, off_rew, lds;
+  int off_map, off_dep, off_bits, off_feat, off_pos, off_rew, off_stage, lds;  // off_stage < 0: none
   int win, K, D, limit, hw;          // window, knn, obs dim, episode limit, H*W
   double move_rew, stay_rew, stay_goal_rew, nc_rew, ec_rew, env_rew;
   int sq_max, bonus_len;             // LUT sizes
@@ -425,13 +425,14 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
     posL[ag] = make_int2(r, c);
   }
   wave_fence();
+  constexpr int WW = WIN * WIN;
+  constexpr int DF = (KF > 0 && LF > 0) ? 2 * WW + NF * KF : 1;  // fast-path row length
+  float o[DF];
   if (has && a.obs) {
     float* kn;
-    constexpr int WW = WIN * WIN;
     if constexpr (KF > 0 && LF > 0) {
-      // -------- fast path: the whole row in registers, merged dwordx4 stores --------
-      constexpr int D = 2 * WW + NF * KF;
-      float o[D];
+      // -------- fast path: the whole row in registers --------
+      constexpr int D = DF;
       if constexpr (WIN > 0) {  // window planes (:327-342) from whole map words
         const int wb = (cur - H2 * pitch - H2);
         const int sh = (wb & 3) * 8;
@@ -493,9 +494,11 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
           for (int q = 0; q < NF; ++q) row[q] = -1.0f;
         }
       }
-      uint32_t* d = (uint32_t*)(a.obs + oa * D);
+      if (g.off_stage < 0) {  // rows straight to HBM (per-lane dword stores)
+        uint32_t* d = (uint32_t*)(a.obs + oa * D);
 #pragma unroll
-      for (int i = 0; i < D; ++i) d[i] = __float_as_uint(o[i]);
+        for (int i = 0; i < D; ++i) d[i] = __float_as_uint(o[i]);
+      }
     } else {
       // -------- generic path --------
       float* o = a.obs + oa * g.D;
@@ -539,6 +542,51 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
     }
     (void)kn;
   }
+  if constexpr (KF > 0 && LF > 0) {
+    // The rows of a half wave (32 lanes = whole envs, or half of one 64-agent env) are
+    // one contiguous run of the obs tensor: stage them in LDS as its byte image (at
+    // the run's own 16-byte misalignment) and copy the run with lane-contiguous
+    // 16-byte stores -- per-lane dword stores of 460-byte rows touch 64 lines each.
+    if (a.obs && g.off_stage >= 0) {
+      constexpr int D = DF;
+      unsigned char* stage = lds + g.off_stage;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        long long rec0;
+        int nrec;
+        if (g.L == 64) {
+          rec0 = (long long)(blockIdx.x * g.EPW) * N + 32 * hh;
+          nrec = (blockIdx.x * g.EPW < g.E) ? max(0, min(N - 32 * hh, 32)) : 0;
+        } else {
+          const int s0 = (32 * hh) >> g.lshift;  // first env slot of the half
+          const int e0 = blockIdx.x * g.EPW + s0;
+          rec0 = (long long)e0 * N;
+          nrec = max(0, min(min(32 >> g.lshift, g.EPW - s0), g.E - e0)) * N;
+        }
+        if (nrec == 0) continue;
+        unsigned char* gdst = (unsigned char*)(a.obs + rec0 * D);
+        const uint32_t mis = (uint32_t)(uintptr_t)gdst & 15u;
+        if (has && (lane64 >> 5) == hh) {
+          uint32_t* row = (uint32_t*)(stage + mis + (size_t)(oa - rec0) * (D * 4));
+#pragma unroll
+          for (int i = 0; i < D; ++i) row[i] = __float_as_uint(o[i]);
+        }
+        wave_fence();
+        const int nbytes = nrec * D * 4;
+        const int head = mis ? min(16 - (int)mis, nbytes) : 0;  // a multiple of 4
+        const int body = (nbytes - head) & ~15;
+        if (lane64 < head / 4) ((uint32_t*)gdst)[lane64] = ((const uint32_t*)(stage + mis))[lane64];
+        const uint4* s4 = (const uint4*)(stage + mis + head);  // 16-byte aligned: mis + head
+        uint4* g4 = (uint4*)(gdst + head);
+        for (int i = lane64; i < body / 16; i += 64) g4[i] = s4[i];
+        const int tail = nbytes - head - body;
+        if (lane64 < tail / 4)
+          ((uint32_t*)(gdst + head + body))[lane64] = ((const uint32_t*)(stage + mis + head + body))[lane64];
+        wave_fence();  // the next half's rows reuse the image
+      }
+    }
+  }
+  (void)o;
   // avail (:399-433): neighbour in bounds and not a free-standing obstacle
   if (has && a.avail) {
     uint32_t m = 16u;
@@ -732,6 +780,15 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.off_feat = off; off += EPW * g.feat_env_bytes;
   g.off_pos = off; off += EPW * 64 * 8;
   g.off_rew = off; off += EPW * g.rew_env_bytes;
+  // the fast observation path's staging image: 32 rows + 16 bytes of alignment slack
+  g.off_stage = -1;
+  if (g.K == 5 && (g.win == 3 || g.win == 5 || g.win == 7) && L >= 8 && L <= 32) {
+    const int st = round_up(32 * g.D * 4 + 16, 16);
+    if (off + st <= 64 * 1024) {
+      g.off_stage = off;
+      off += st;
+    }
+  }
   g.lds = off;
   if (g.lds > 64 * 1024) {
     int rc0 = MAPFX_OK;

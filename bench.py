@@ -68,9 +68,13 @@ def parse():
                     help="CPU/gloo rehearsal of the multi-rank launch + shard + packed gather")
     ap.add_argument("--selftest-envs", type=int, default=6)
     ap.add_argument("--pmc", default=None, help="PMC summary (default profiles/pmc_<config>.json)")
-    ap.add_argument("--env", default="mapf_grid", choices=("mapf_grid", "marl_partial", "runner"),
+    ap.add_argument("--env", default="mapf_grid",
+                    choices=("mapf_grid", "marl_partial", "runner", "primal"),
                     help="mapf_grid: the BASELINE.json metric (default); marl_partial: the "
-                         "SURVEY §8(f) F1 env on its yaml config, one launch per step")
+                         "SURVEY §8(f) F1 env on its yaml config, one launch per step; runner: "
+                         "F2 batched ParallelRunner episodes; primal: F3 sequential dynamics")
+    ap.add_argument("--primal-envs", type=int, default=4096)
+    ap.add_argument("--primal-calls", type=int, default=64, help="_step calls per world per launch")
     ap.add_argument("--partial-envs", type=int, default=4096)
     return ap.parse_args()
 
@@ -205,6 +209,8 @@ def main():
         return run_partial(args, dist, rank, world, local)
     if args.env == "runner":
         return run_runner(args, dist, rank, world, local)
+    if args.env == "primal":
+        return run_primal(args, dist, rank, world, local)
     S, N, E, p, shared = CONFIGS[args.config]
     W = args.window
     K, WU = args.steps, args.warmup
@@ -570,6 +576,99 @@ def run_partial(args, dist, rank, world, local):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None, "bytes_per_env_step": bpes},
+            "cpu_baseline": cpu}), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def primal_bytes_per_call(s):
+    """Algorithmic HBM bytes of one PRIMAL `_step((agent_id, action))` call
+    (SURVEY §8(f) F3): agent id + action read (8), reward f64 + done + next mask +
+    on_goal + valid (12), the 4 x s x s observation maps (u8) and the f64 goal vector (24)."""
+    return 8 + 12 + 4 * s * s + 24
+
+
+def run_primal(args, dist, rank, world, local):
+    """PRIMAL sequential dynamics (envs/mapf_primal.py:549-637): E
+    worlds of 32 x 32 (10 % obstacles) with 16 agents and observation_size 10 per GPU;
+    each launch makes `--primal-calls` single-agent `_step` calls per world, in order
+    (agents round robin, random actions), every call's observation written."""
+    import mapfx
+    from mapfx.maps import synthetic_instances
+    S, N, s_obs, E, KC = 32, 16, 10, args.primal_envs, args.primal_calls
+    offset = rank * E
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.10, seed=1, env_offset=offset)
+    b = mapfx.PrimalBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                          observation_size=s_obs, device="cuda:%d" % local)
+    rng = np.random.default_rng(7 + rank)
+    ids = torch.from_numpy(np.tile((np.arange(KC) % N + 1).astype(np.int32), (E, 1))).cuda()
+    acts = torch.from_numpy(rng.integers(0, 5, size=(E, KC)).astype(np.int32)).cuda()
+    R = max(1, args.steps // KC)          # launches timed
+    RW = max(1, args.warmup // KC)
+    for _ in range(RW):
+        b.act(ids, acts)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    e1.record(stream)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(R):
+        b.act(ids, acts)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    kern_ms = e0.elapsed_time(e1) / R
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    b.check_err()
+    calls = E * world * KC * R
+    bpc = primal_bytes_per_call(s_obs)
+    launch_bytes = E * (KC * bpc + (8 + 8 + 8) * N + inst["bits"].shape[1])  # + pos/goal in, pos out
+    achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        from oracle.primal_dyn_oracle import PrimalWorld
+        ids_h, acts_h = ids.cpu().numpy(), acts.cpu().numpy()
+        t_start, n, e = time.perf_counter(), 0, 0
+        while time.perf_counter() - t_start < args.cpu_seconds:
+            we = e % E
+            w = PrimalWorld(inst["grid"][we % inst["grid"].shape[0]], inst["init_pos"][we],
+                            inst["goals"][we], s_obs)
+            for k in range(KC):
+                w.step(int(ids_h[we, k]) - 1, int(acts_h[we, k]))
+            n += KC
+            e += 1
+        el_c = time.perf_counter() - t_start
+        cpu = {"value": round(n / el_c, 1), "unit": "agent-calls/s", "cores": 1, "kind": "port",
+               "sample": "%d calls (%d worlds x %d) of the same workload: "
+                         "oracle/primal_dyn_oracle.py PrimalWorld.step, %.1f s" % (n, e, KC, el_c)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "PRIMAL _step calls/sec (sequential single-agent dynamics + observation)",
+            "value": round(calls / elapsed, 1), "unit": "agent-calls/s",
+            "n_gpus": world, "steps": KC * R, "warmup": KC * RW,
+            "ms_per_step": round(elapsed / (KC * R) * 1e3, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int32+f64+u8",
+            "data": "synthetic (32x32 maps, 10% obstacles, distinct free starts/goals; agents "
+                    "round robin, uniform random actions in HBM)",
+            "config": {"workload": "primal: %d worlds/GPU of 32x32, %d agents, observation_size "
+                                   "%d, %d _step calls per world per launch (%d launches)"
+                                   % (E, N, s_obs, KC, R),
+                       "envs_total": E * world, "agents": N, "parallelism": "env-shard x%d" % world},
+            "kernel_ms_per_launch": round(kern_ms, 5),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None, "bytes_per_call": bpc, "bytes_per_launch": int(launch_bytes)},
             "cpu_baseline": cpu}), flush=True)
     if dist:
         dist.barrier()

@@ -2,11 +2,18 @@
 #ifndef MAPFX_INTERNAL_H
 #define MAPFX_INTERNAL_H
 
+#include "mapfx_partial.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
 // sets the message returned by mapfx_last_error(); returns `code`
 int mapfx_internal_error(int code, const char* msg);
+// partial.hip: mapfx_partial_step with the observation rows written to an EpisodeBatch
+// time row (obs_rows + e * obs_env_stride floats, only envs with obs_mask[e] != 0)
+int mapfx_partial_step_rows(mapfx_partial_t* h, const mapfx_partial_state* st, const void* actions,
+                            int action_dtype, const mapfx_partial_out* out, float* obs_rows,
+                            long long obs_env_stride, const uint8_t* obs_mask, void* stream);
 #ifdef __cplusplus
 }
 #endif

@@ -44,7 +44,7 @@ struct PGeo {
   int P, pl, pitch, rows, wpr;       // padded LDS map
   int bits_words, map_shared;
   long long map_stride;
-  int map_env_bytes, bits_env_bytes, feat_env_bytes, rew_env_bytes;
+  int map_env_bytes, bits_env_bytes, feat_env_bytes, rew_env_bytes, stage_env_bytes;
   int off_map, off_dep, off_bits, off_feat, off_pos, off_rew, off_stage, lds;  // off_stage < 0: none
   int win, K, D, limit, hw;          // window, knn, obs dim, episode limit, H*W
   double move_rew, stay_rew, stay_goal_rew, nc_rew, ec_rew, env_rew;
@@ -78,7 +78,19 @@ struct PArgs {
   int32_t* err;
   const double* sqrt_lut;   // sqrt(n), n = 0 .. sq_max
   const double* bonus_lut;  // (complete / gamma ** (limit - t)) * fac, t = 0 .. bonus_len-1
+  // runner fusion (mapfx_partial_step_rows): observation rows go to obs_rows + e *
+  // obs_env_stride (an EpisodeBatch time row) for the envs with obs_mask[e] != 0,
+  // instead of the contiguous `obs`
+  float* obs_rows;
+  long long obs_env_stride;
+  const uint8_t* obs_mask;
 };
+
+// where env e's observation rows go ([N][D] floats), or nullptr when not written
+__device__ __forceinline__ float* obs_env(const PArgs& a, int e, int D, int N) {
+  if (a.obs_rows) return (a.obs_mask && !a.obs_mask[e]) ? nullptr : a.obs_rows + (long long)e * a.obs_env_stride;
+  return a.obs ? a.obs + (long long)e * N * D : nullptr;
+}
 
 __device__ inline int load_act(const void* p, int dtype, long long idx) {
   if (dtype == MAPFX_I8) return (int)((const int8_t*)p)[idx];
@@ -428,7 +440,8 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   constexpr int WW = WIN * WIN;
   constexpr int DF = (KF > 0 && LF > 0) ? 2 * WW + NF * KF : 1;  // fast-path row length
   float o[DF];
-  if (has && a.obs) {
+  float* const my_obs = env_ok ? obs_env(a, env, (KF > 0 && LF > 0) ? DF : g.D, N) : nullptr;
+  if (has && my_obs) {
     float* kn;
     if constexpr (KF > 0 && LF > 0) {
       // -------- fast path: the whole row in registers --------
@@ -495,13 +508,13 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
         }
       }
       if (g.off_stage < 0) {  // rows straight to HBM (per-lane dword stores)
-        uint32_t* d = (uint32_t*)(a.obs + oa * D);
+        uint32_t* d = (uint32_t*)(my_obs + ag * D);
 #pragma unroll
         for (int i = 0; i < D; ++i) d[i] = __float_as_uint(o[i]);
       }
     } else {
       // -------- generic path --------
-      float* o = a.obs + oa * g.D;
+      float* o = my_obs + ag * g.D;
       if constexpr (WIN > 0) {  // window planes (:327-342): OOB / obstacle -> 1; agents -> count
         for (int y = 0; y < WIN; ++y) {
           for (int x = 0; x < WIN; ++x) {
@@ -543,46 +556,64 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
     (void)kn;
   }
   if constexpr (KF > 0 && LF > 0) {
-    // The rows of a half wave (32 lanes = whole envs, or half of one 64-agent env) are
-    // one contiguous run of the obs tensor: stage them in LDS as its byte image (at
-    // the run's own 16-byte misalignment) and copy the run with lane-contiguous
-    // 16-byte stores -- per-lane dword stores of 460-byte rows touch 64 lines each.
-    if (a.obs && g.off_stage >= 0) {
+    // The rows of an env in a half wave (32 lanes = whole envs, or half of one
+    // 64-agent env) are one contiguous run of the destination: stage each run in LDS
+    // as its byte image (at the run's own 16-byte misalignment) and copy it with
+    // lane-contiguous 16-byte stores -- per-lane dword stores of 460-byte rows touch
+    // 64 lines each.
+    if ((a.obs || a.obs_rows) && g.off_stage >= 0) {
       constexpr int D = DF;
-      unsigned char* stage = lds + g.off_stage;
+      const int SE = g.stage_env_bytes;  // one env's run + 16 bytes of alignment slack
+      const int blk = (int)blockIdx.x;   // (unsigned blockIdx would make g.E - ... unsigned)
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
-        long long rec0;
-        int nrec;
+        // envs of this half: slots s0 .. s0 + ne - 1, runs of nr records from agent a0
+        int s0, ne, a0, nr;
         if (g.L == 64) {
-          rec0 = (long long)(blockIdx.x * g.EPW) * N + 32 * hh;
-          nrec = (blockIdx.x * g.EPW < g.E) ? max(0, min(N - 32 * hh, 32)) : 0;
+          s0 = 0;
+          ne = (blk * g.EPW < g.E) ? 1 : 0;
+          a0 = 32 * hh;
+          nr = max(0, min(N - 32 * hh, 32));
         } else {
-          const int s0 = (32 * hh) >> g.lshift;  // first env slot of the half
-          const int e0 = blockIdx.x * g.EPW + s0;
-          rec0 = (long long)e0 * N;
-          nrec = max(0, min(min(32 >> g.lshift, g.EPW - s0), g.E - e0)) * N;
+          s0 = (32 * hh) >> g.lshift;
+          ne = max(0, min(min(32 >> g.lshift, g.EPW - s0), g.E - (blk * g.EPW + s0)));  // signed
+          a0 = 0;
+          nr = N;
         }
-        if (nrec == 0) continue;
-        unsigned char* gdst = (unsigned char*)(a.obs + rec0 * D);
-        const uint32_t mis = (uint32_t)(uintptr_t)gdst & 15u;
-        if (has && (lane64 >> 5) == hh) {
-          uint32_t* row = (uint32_t*)(stage + mis + (size_t)(oa - rec0) * (D * 4));
+        if (ne == 0 || nr == 0) continue;
+        // contiguous destination (a.obs): the half's envs are ONE run; EpisodeBatch rows
+        // (a.obs_rows): one run per env
+        const bool one_run = a.obs_rows == nullptr;
+        const int nrun = one_run ? 1 : ne;
+        const int kme = slot - s0;  // this lane's env within the half
+        if (has && (lane64 >> 5) == hh && my_obs) {
+          const int k = one_run ? 0 : kme;
+          const float* rb = one_run ? obs_env(a, blk * g.EPW + s0, D, N) : my_obs + a0 * D;
+          const uint32_t mis = (uint32_t)(uintptr_t)rb & 15u;
+          const int ri = (one_run ? kme * N : 0) + ag - a0;  // row within the run
+          uint32_t* row = (uint32_t*)(lds + g.off_stage + k * SE + mis + ri * (D * 4));
 #pragma unroll
           for (int i = 0; i < D; ++i) row[i] = __float_as_uint(o[i]);
         }
         wave_fence();
-        const int nbytes = nrec * D * 4;
-        const int head = mis ? min(16 - (int)mis, nbytes) : 0;  // a multiple of 4
-        const int body = (nbytes - head) & ~15;
-        if (lane64 < head / 4) ((uint32_t*)gdst)[lane64] = ((const uint32_t*)(stage + mis))[lane64];
-        const uint4* s4 = (const uint4*)(stage + mis + head);  // 16-byte aligned: mis + head
-        uint4* g4 = (uint4*)(gdst + head);
-        for (int i = lane64; i < body / 16; i += 64) g4[i] = s4[i];
-        const int tail = nbytes - head - body;
-        if (lane64 < tail / 4)
-          ((uint32_t*)(gdst + head + body))[lane64] = ((const uint32_t*)(stage + mis + head + body))[lane64];
-        wave_fence();  // the next half's rows reuse the image
+        for (int k = 0; k < nrun; ++k) {
+          float* eo = obs_env(a, blk * g.EPW + s0 + k, D, N);
+          if (!eo) continue;
+          unsigned char* gdst = (unsigned char*)(eo + a0 * D);
+          const uint32_t mis = (uint32_t)(uintptr_t)gdst & 15u;
+          const unsigned char* img = lds + g.off_stage + k * SE + mis;
+          const int nbytes = (one_run ? ne : 1) * nr * D * 4;
+          const int head = mis ? min(16 - (int)mis, nbytes) : 0;  // a multiple of 4
+          const int body = (nbytes - head) & ~15;
+          if (lane64 < head / 4) ((uint32_t*)gdst)[lane64] = ((const uint32_t*)img)[lane64];
+          const uint4* s4 = (const uint4*)(img + head);  // 16-byte aligned: mis + head
+          uint4* g4 = (uint4*)(gdst + head);
+          for (int i = lane64; i < body / 16; i += 64) g4[i] = s4[i];
+          const int tail = nbytes - head - body;
+          if (lane64 < tail / 4)
+            ((uint32_t*)(gdst + head + body))[lane64] = ((const uint32_t*)(img + head + body))[lane64];
+        }
+        wave_fence();  // the next half's rows reuse the images
       }
     }
   }
@@ -782,8 +813,9 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.off_rew = off; off += EPW * g.rew_env_bytes;
   // the fast observation path's staging image: 32 rows + 16 bytes of alignment slack
   g.off_stage = -1;
+  g.stage_env_bytes = round_up(std::min(L, 32) * g.D * 4 + 16, 16);
   if (g.K == 5 && (g.win == 3 || g.win == 5 || g.win == 7) && L >= 8 && L <= 32) {
-    const int st = round_up(32 * g.D * 4 + 16, 16);
+    const int st = (32 / std::min(L, 32)) * g.stage_env_bytes;
     if (off + st <= 64 * 1024) {
       g.off_stage = off;
       off += st;
@@ -885,6 +917,31 @@ int mapfx_partial_step(mapfx_partial_t* h, const mapfx_partial_state* st, const 
   memset(&a, 0, sizeof(a));
   fill_state(a, st);
   fill_out(a, out);
+  a.actions = actions;
+  a.act_dtype = action_dtype;
+  a.do_step = 1;
+  return launch(h, a, stream);
+}
+
+// mapfx_partial_step with the observation rows written to an EpisodeBatch time row
+// (obs_rows + e * obs_env_stride floats, envs with obs_mask[e] != 0) instead of
+// out->obs: the runner's fused step (runner.hip), internal.h
+int mapfx_partial_step_rows(mapfx_partial_t* h, const mapfx_partial_state* st, const void* actions,
+                            int action_dtype, const mapfx_partial_out* out, float* obs_rows,
+                            long long obs_env_stride, const uint8_t* obs_mask, void* stream) {
+  if (!h) return perr(MAPFX_EINVAL, "NULL handle");
+  int rc = check_state(h, st);
+  if (rc) return rc;
+  if (!actions) return perr(MAPFX_EINVAL, "NULL actions");
+  if (action_dtype < MAPFX_I8 || action_dtype > MAPFX_I64) return perr(MAPFX_EINVAL, "bad action_dtype");
+  PArgs a;
+  memset(&a, 0, sizeof(a));
+  fill_state(a, st);
+  fill_out(a, out);
+  a.obs = nullptr;
+  a.obs_rows = obs_rows;
+  a.obs_env_stride = obs_env_stride;
+  a.obs_mask = obs_mask;
   a.actions = actions;
   a.act_dtype = action_dtype;
   a.do_step = 1;

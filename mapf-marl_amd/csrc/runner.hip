@@ -236,8 +236,19 @@ int mapfx_runner_step(mapfx_partial_t* h, const mapfx_partial_state* st, const m
                       const mapfx_episode_rows* rows, void* stream) {
   int rc = mapfx_runner_actions(rs, actions, action_dtype, row_stride, ts, rows, stream);
   if (rc) return rc;
-  if ((rc = mapfx_partial_step(h, st, rs->env_actions, MAPFX_I8, out, stream))) return rc;
-  return mapfx_runner_post(rs, st->terminated, out, ts, counts_out, rows, stream);
+  if (!rows || !rows->obs)
+    return (rc = mapfx_partial_step(h, st, rs->env_actions, MAPFX_I8, out, stream))
+               ? rc : mapfx_runner_post(rs, st->terminated, out, ts, counts_out, rows, stream);
+  // fused: the env step writes the observation rows of the envs running before it
+  // (rs->alive, updated only by the post kernel) straight into the batch's time row
+  // ts + 1, so the post kernel moves no observation bytes
+  float* obs_row = ts + 1 < rows->max_t ? rows->obs + (int64_t)(ts + 1) * rows->obs_st : nullptr;
+  if ((rc = mapfx_partial_step_rows(h, st, rs->env_actions, MAPFX_I8, out, obs_row, rows->obs_sb,
+                                    rs->alive, stream)))
+    return rc;
+  mapfx_episode_rows r2 = *rows;
+  r2.obs = nullptr;
+  return mapfx_runner_post(rs, st->terminated, out, ts, counts_out, &r2, stream);
 }
 
 int mapfx_host_ring_alloc(int32_t n, int32_t** host_ptr, int32_t** dev_ptr) {

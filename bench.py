@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--dist-selftest", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank launch + shard + packed gather")
     ap.add_argument("--selftest-envs", type=int, default=6)
+    ap.add_argument("--rehearse-shared-gpu", action="store_true",
+                    help="rehearsal of the N-rank path on a one-GPU box: every rank on cuda:0, "
+                         "collectives over gloo (never a scaling number)")
     ap.add_argument("--pmc", default=None, help="PMC summary (default profiles/pmc_<config>.json)")
     ap.add_argument("--env", default="mapf_grid",
                     choices=("mapf_grid", "marl_partial", "runner", "primal"),
@@ -183,10 +186,13 @@ def dist_selftest(args, rank, world):
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:], need_gpus=not args.dist_selftest))
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:],
+                              need_gpus=not (args.dist_selftest or args.rehearse_shared_gpu)))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse_shared_gpu:
+        local = 0
     if world != args.gpus:
         print("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus), file=sys.stderr)
         sys.exit(2)
@@ -200,7 +206,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse_shared_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import mapfx
     from mapfx.maps import synthetic_instances, warehouse_grid
@@ -406,7 +415,9 @@ def main():
                                       if wkind == "window_occ" else "", T, len(plans),
                                       "" if len(plans) == 1 else "es"),
                        "envs_total": total_envs, "agents": N, "grid": [S, S], "chunk_T": T,
-                       "parallelism": "env-shard x%d" % world},
+                       "parallelism": "env-shard x%d" % world
+                       + (" (REHEARSAL: all ranks on cuda:0 over gloo)" if args.rehearse_shared_gpu
+                          else "")},
             "env_steps_per_s": round(total_envs * K / elapsed, 1),
             "kernel_ms_per_launch": round(kern_ms, 5),
             "timing": {"wall_ms": round(elapsed * 1e3, 4),

@@ -269,12 +269,13 @@ def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T, obs, win):
     (4096, 64, 5, False, 16),   # the bench shape
     (256, 1, 5, False, 16), (256, 2, 5, False, 16), (256, 3, 3, False, 16), (252, 17, 7, False, 16),
     (64, 40, 5, True, 16),
-    (250, 12, 5, False, 12), (130, 9, 3, True, 7), (66, 10, 5, False, 40)])  # N < L: generic lanes
+    (250, 12, 5, False, 12), (130, 9, 3, True, 7), (66, 10, 5, False, 40),  # N < L
+    (130, 12, 5, False, 64), (64, 40, 3, True, 64), (40, 9, 7, False, 64)])  # 64-agent store wave
 def test_runner_rollout_every_step(mapfx_mod, E, T, win, autoreset, N):
     """Runner rollouts (every PyMARL output, no full map; N = 16 takes the store-wave
     kernel): each step's outputs must equal one step launch's, step by step."""
     from mapfx.maps import synthetic_instances
-    S = 32 if not autoreset else 8
+    S = 32 if not autoreset else (8 if N <= 16 else 12)
     inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=12)
     kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=2000 if not autoreset else 9,
               obs=("window",), window=win)

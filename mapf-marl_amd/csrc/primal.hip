@@ -89,12 +89,45 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
   wave_fence();
   const auto is_obst = [&](int r, int c) { const int i = r * W + c; return (obst[i >> 5] >> (i & 31)) & 1u; };
 
+  // the calls' (agent id, action) pairs: lane l holds call 64 b + l of block b, the
+  // next block is loaded while this one runs, and each call reads its pair with
+  // v_readlane (uniform index) -- no HBM round trip inside the sequential loop
+  const long long e0k = (long long)e * a.K;
+  int id_c = 0, act_c = 0, id_n = 0, act_n = 0;
+  if (lane < a.K) {
+    id_n = a.ids[e0k + lane];
+    act_n = a.acts[e0k + lane];
+  }
+  int pend_dx = 0, pend_dy = 0;
+  const auto flush_vec = [&](int kb, int n) {  // calls kb .. kb + n - 1, one per lane
+    if (lane < n) {
+      const long long ekl = e0k + kb + lane;
+      const double mag = a.pow_lut[pend_dx * pend_dx + pend_dy * pend_dy];
+      double vx = (double)pend_dx, vy = (double)pend_dy;
+      if (mag != 0.0) {
+        vx = vx / mag;
+        vy = vy / mag;
+      }
+      a.vec[ekl * 3 + 0] = vx;
+      a.vec[ekl * 3 + 1] = vy;
+      a.vec[ekl * 3 + 2] = mag;
+    }
+  };
   for (int k = 0; k < a.K; ++k) {
-    const long long ek = (long long)e * a.K + k;
-    const int aid = a.ids[ek] - 1;
-    const int act = a.acts[ek];
+    const long long ek = e0k + k;
+    if ((k & 63) == 0) {
+      id_c = id_n;
+      act_c = act_n;
+      if (k + 64 + lane < a.K) {
+        id_n = a.ids[ek + 64 + lane];
+        act_n = a.acts[ek + 64 + lane];
+      }
+    }
+    const int aid = __builtin_amdgcn_readlane(id_c, k & 63) - 1;
+    const int act = __builtin_amdgcn_readlane(act_c, k & 63);
     if (aid < 0 || aid >= N || act < 0 || act > 4) {  // the reference asserts (:556-558)
       if (lane == 0 && a.err) atomicCAS(a.err, 0, e + 1);
+      if (a.vec && (k & 63)) flush_vec(k & ~63, k & 63);  // the block's earlier calls
       break;
     }
     // ---- State.moveAgent (:103-135), lane 0 ----
@@ -183,19 +216,15 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
       if (a.next_mask) a.next_mask[ek] = (uint8_t)m;
       if (a.on_goal) a.on_goal[ek] = (ax == gg.x && ay == gg.y) ? 1 : 0;
       if (a.valid) a.valid[ek] = status >= 0 ? 1 : 0;
-      if (a.vec) {  // :379-384
-        const int dx = gg.x - ax, dy = gg.y - ay;
-        const double mag = a.pow_lut[dx * dx + dy * dy];
-        double vx = (double)dx, vy = (double)dy;
-        if (mag != 0.0) {
-          vx = vx / mag;
-          vy = vy / mag;
-        }
-        a.vec[ek * 3 + 0] = vx;
-        a.vec[ek * 3 + 1] = vy;
-        a.vec[ek * 3 + 2] = mag;
-      }
     }
+    // goal vector (:379-384): its magnitude needs a LUT load, so lane k & 63 keeps the
+    // call's (dx, dy) and the wave writes a block's 64 vectors together (one load
+    // latency per 64 calls instead of one per call on the sequential path)
+    if (lane == (k & 63)) {
+      pend_dx = gg.x - ax;
+      pend_dy = gg.y - ay;
+    }
+    if (a.vec && ((k & 63) == 63 || k + 1 == a.K)) flush_vec(k & ~63, (k & 63) + 1);
     wave_fence();
   }
   wave_fence();

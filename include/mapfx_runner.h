@@ -88,8 +88,11 @@ int mapfx_runner_post(const mapfx_runner_state* rs, const uint8_t* terminated,
                       const mapfx_partial_out* out, int32_t ts, int32_t* counts_out,
                       const mapfx_episode_rows* rows, void* stream);
 
-/* One runner step in one call: mapfx_runner_actions, mapfx_partial_step(h, st,
- * rs->env_actions, MAPFX_I8, out), mapfx_runner_post(rs, st->terminated, out, ...). */
+/* One runner step in one call: mapfx_runner_actions, the env step of
+ * mapfx_partial_step(h, st, rs->env_actions, MAPFX_I8, out) and mapfx_runner_post(rs,
+ * st->terminated, out, ...).  When rows->obs is set, the env step writes the
+ * observation rows of the envs running before it straight into rows->obs at ts + 1
+ * (out->obs is then not written) and the post kernel copies no observation bytes. */
 int mapfx_runner_step(mapfx_partial_t* h, const mapfx_partial_state* st, const mapfx_partial_out* out,
                       const mapfx_runner_state* rs, const void* actions, int32_t action_dtype,
                       int64_t row_stride, int32_t ts, int32_t* counts_out,

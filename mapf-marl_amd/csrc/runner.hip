@@ -136,43 +136,53 @@ __global__ void __launch_bounds__(RB) runner_post_kernel(mapfx_runner_state rs, 
 
 // envs_not_terminated (:123) for the next MAC call: ascending indices of alive_prev,
 // padded with the first one (so a MAC indexing rows by `bs` only sees running envs);
-// counts = {len(bs), number alive}.  One workgroup: per-thread chunk counts, scan.
+// counts = {len(bs), number alive}.  One workgroup: per-thread chunk counts, a
+// shuffle scan inside each wave and one barrier for the 16 wave totals.
 constexpr int CT = 1024;
 __global__ void __launch_bounds__(CT) runner_compact_kernel(mapfx_runner_state rs, int32_t* counts_out) {
-  __shared__ int part[CT];
-  __shared__ int alive_part[CT];
+  __shared__ int wsum[CT / 64];
+  __shared__ int wsum_a[CT / 64];
   const int chunk = (rs.B + CT - 1) / CT;
   const int lo = threadIdx.x * chunk, hi = min(rs.B, lo + chunk);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int c = 0, ca = 0;
   for (int b = lo; b < hi; ++b) {
     c += rs.alive_prev[b] ? 1 : 0;
     ca += rs.alive[b] ? 1 : 0;
   }
-  part[threadIdx.x] = c;
-  alive_part[threadIdx.x] = ca;
-  __syncthreads();
-  for (int off = 1; off < CT; off <<= 1) {  // inclusive scan (Hillis-Steele)
-    const int v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-    const int va = threadIdx.x >= off ? alive_part[threadIdx.x - off] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    alive_part[threadIdx.x] += va;
-    __syncthreads();
+  int x = c;  // inclusive scan over the wave's lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
   }
-  int o = part[threadIdx.x] - c;
+  int xa = ca;  // the wave's alive count
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) xa += __shfl_xor(xa, o);
+  if (lane == 63) wsum[wv] = x;
+  if (lane == 0) wsum_a[wv] = xa;
+  __syncthreads();
+  int off = 0, total = 0, total_a = 0;
+#pragma unroll
+  for (int i = 0; i < CT / 64; ++i) {
+    const int v = wsum[i];
+    off += i < wv ? v : 0;
+    total += v;
+    total_a += wsum_a[i];
+  }
+  int o = off + x - c;  // exclusive prefix of this thread's chunk
   for (int b = lo; b < hi; ++b)
     if (rs.alive_prev[b]) rs.bs[o++] = b;
-  const int total = part[CT - 1];
   __syncthreads();  // bs[0] written
   const int64_t first = total > 0 ? rs.bs[0] : 0;
   for (int j = total + threadIdx.x; j < rs.B; j += CT) rs.bs[j] = first;
   if (threadIdx.x == 0) {
     rs.counts[0] = total;
-    rs.counts[1] = alive_part[CT - 1];
+    rs.counts[1] = total_a;
     rs.env_steps[0] += total;  // the envs stepped this step: env_steps_this_run (:142)
     if (counts_out) {  // possibly pinned host memory
       counts_out[0] = total;
-      counts_out[1] = alive_part[CT - 1];
+      counts_out[1] = total_a;
     }
   }
 }

@@ -32,6 +32,10 @@
 #include "mapfx.h"
 #include "mapfx_partial.h"
 
+#ifndef PABL
+#define PABL 0  // diagnostic builds only: 1 skip the obs rows, 2 skip the step, 4 skip the staged copy
+#endif
+
 namespace {
 
 constexpr int NF = 13;   // KNN features per agent (:81)
@@ -44,7 +48,7 @@ struct PGeo {
   int P, pl, pitch, rows, wpr;       // padded LDS map
   int bits_words, map_shared;
   long long map_stride;
-  int map_env_bytes, bits_env_bytes, feat_env_bytes, rew_env_bytes, stage_env_bytes;
+  int map_env_bytes, bits_env_bytes, feat_env_bytes, rew_env_bytes, stage_env_bytes, stage_lanes;
   int off_map, off_dep, off_bits, off_feat, off_pos, off_rew, off_stage, lds;  // off_stage < 0: none
   int win, K, D, limit, hw;          // window, knn, obs dim, episode limit, H*W
   double move_rew, stay_rew, stay_goal_rew, nc_rew, ec_rew, env_rew;
@@ -324,7 +328,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   wave_fence();
 
   // ---- step (:165-310) ----
-  if (a.do_step && env_ok) {
+  if (a.do_step && env_ok && !(PABL & 2)) {
     int act = 4;
     if (has) {
       act = load_act(a.actions, a.act_dtype, oa);
@@ -441,7 +445,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   constexpr int DF = (KF > 0 && LF > 0) ? 2 * WW + NF * KF : 1;  // fast-path row length
   float o[DF];
   float* const my_obs = env_ok ? obs_env(a, env, (KF > 0 && LF > 0) ? DF : g.D, N) : nullptr;
-  if (has && my_obs) {
+  if (has && my_obs && !(PABL & 1)) {
     float* kn;
     if constexpr (KF > 0 && LF > 0) {
       // -------- fast path: the whole row in registers --------
@@ -556,64 +560,77 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
     (void)kn;
   }
   if constexpr (KF > 0 && LF > 0) {
-    // The rows of an env in a half wave (32 lanes = whole envs, or half of one
-    // 64-agent env) are one contiguous run of the destination: stage each run in LDS
-    // as its byte image (at the run's own 16-byte misalignment) and copy it with
-    // lane-contiguous 16-byte stores -- per-lane dword stores of 460-byte rows touch
-    // 64 lines each.
-    if ((a.obs || a.obs_rows) && g.off_stage >= 0) {
+    // The rows of the envs of a staging group (the whole wave, or each half of it) are
+    // one contiguous run of the destination (a.obs), or one run per env (EpisodeBatch
+    // rows): stage each run in LDS as its byte image, at the run's own 16-byte
+    // misalignment, and copy it with lane-contiguous 16-byte stores -- per-lane dword
+    // stores of 460-byte rows touch 64 lines each.  The images alias the LDS regions
+    // the step and the observation rows are done with (dep onwards; the rows are in
+    // registers by now).
+    if ((a.obs || a.obs_rows) && g.off_stage >= 0 && !(PABL & 4)) {
       constexpr int D = DF;
-      const int SE = g.stage_env_bytes;  // one env's run + 16 bytes of alignment slack
+      const int G = g.stage_lanes;       // 64 or 32
+      const int SE = g.stage_env_bytes;  // one env's rows + 16 bytes of alignment slack
       const int blk = (int)blockIdx.x;   // (unsigned blockIdx would make g.E - ... unsigned)
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        // envs of this half: slots s0 .. s0 + ne - 1, runs of nr records from agent a0
-        int s0, ne, a0, nr;
-        if (g.L == 64) {
-          s0 = 0;
-          ne = (blk * g.EPW < g.E) ? 1 : 0;
-          a0 = 32 * hh;
-          nr = max(0, min(N - 32 * hh, 32));
-        } else {
-          s0 = (32 * hh) >> g.lshift;
-          ne = max(0, min(min(32 >> g.lshift, g.EPW - s0), g.E - (blk * g.EPW + s0)));  // signed
-          a0 = 0;
-          nr = N;
-        }
-        if (ne == 0 || nr == 0) continue;
-        // contiguous destination (a.obs): the half's envs are ONE run; EpisodeBatch rows
-        // (a.obs_rows): one run per env
-        const bool one_run = a.obs_rows == nullptr;
-        const int nrun = one_run ? 1 : ne;
-        const int kme = slot - s0;  // this lane's env within the half
-        if (has && (lane64 >> 5) == hh && my_obs) {
-          const int k = one_run ? 0 : kme;
-          const float* rb = one_run ? obs_env(a, blk * g.EPW + s0, D, N) : my_obs + a0 * D;
+      const bool one_run = a.obs_rows == nullptr;
+      const int run_bytes = N * D * 4;
+      wave_fence();
+      for (int gi = 0; gi < 64 / G; ++gi) {
+        // envs of this group: slots s0 .. s0 + ne - 1
+        const int s0 = (G * gi) >> g.lshift;
+        const int ne = max(0, min(min(G >> g.lshift, g.EPW - s0), g.E - (blk * g.EPW + s0)));  // signed
+        if (ne == 0) break;
+        if (has && my_obs && lane64 / G == gi) {
+          const int kme = slot - s0;  // this lane's env within the group
+          const float* rb = one_run ? a.obs + (long long)(blk * g.EPW + s0) * N * D : my_obs;
           const uint32_t mis = (uint32_t)(uintptr_t)rb & 15u;
-          const int ri = (one_run ? kme * N : 0) + ag - a0;  // row within the run
+          const int k = one_run ? 0 : kme;
+          const int ri = (one_run ? kme * N : 0) + ag;  // row within the run
           uint32_t* row = (uint32_t*)(lds + g.off_stage + k * SE + mis + ri * (D * 4));
 #pragma unroll
           for (int i = 0; i < D; ++i) row[i] = __float_as_uint(o[i]);
         }
         wave_fence();
+        const int nrun = one_run ? 1 : ne;
         for (int k = 0; k < nrun; ++k) {
-          float* eo = obs_env(a, blk * g.EPW + s0 + k, D, N);
-          if (!eo) continue;
-          unsigned char* gdst = (unsigned char*)(eo + a0 * D);
+          unsigned char* gdst;
+          if (one_run) {
+            gdst = (unsigned char*)(a.obs + (long long)(blk * g.EPW + s0) * N * D);
+          } else {  // env s0 + k's destination, from its agent-0 lane (NULL: masked)
+            const uint64_t pe = (uint64_t)(uintptr_t)my_obs;
+            const int src = (s0 + k) << g.lshift;
+            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)pe, src);
+            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(pe >> 32), src);
+            gdst = (unsigned char*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+            if (!gdst) continue;
+          }
           const uint32_t mis = (uint32_t)(uintptr_t)gdst & 15u;
           const unsigned char* img = lds + g.off_stage + k * SE + mis;
-          const int nbytes = (one_run ? ne : 1) * nr * D * 4;
+          const int nbytes = (one_run ? ne : 1) * run_bytes;
           const int head = mis ? min(16 - (int)mis, nbytes) : 0;  // a multiple of 4
           const int body = (nbytes - head) & ~15;
           if (lane64 < head / 4) ((uint32_t*)gdst)[lane64] = ((const uint32_t*)img)[lane64];
           const uint4* s4 = (const uint4*)(img + head);  // 16-byte aligned: mis + head
           uint4* g4 = (uint4*)(gdst + head);
-          for (int i = lane64; i < body / 16; i += 64) g4[i] = s4[i];
+          const int n16 = body / 16;
+          // four LDS reads in flight per lane before their stores
+          for (int i = lane64; i < n16; i += 256) {
+            const bool b1 = i + 64 < n16, b2 = i + 128 < n16, b3 = i + 192 < n16;
+            const uint4 v0 = s4[i];
+            uint4 v1, v2, v3;
+            if (b1) v1 = s4[i + 64];
+            if (b2) v2 = s4[i + 128];
+            if (b3) v3 = s4[i + 192];
+            g4[i] = v0;
+            if (b1) g4[i + 64] = v1;
+            if (b2) g4[i + 128] = v2;
+            if (b3) g4[i + 192] = v3;
+          }
           const int tail = nbytes - head - body;
           if (lane64 < tail / 4)
             ((uint32_t*)(gdst + head + body))[lane64] = ((const uint32_t*)(img + head + body))[lane64];
         }
-        wave_fence();  // the next half's rows reuse the images
+        wave_fence();  // the next group's rows reuse the images
       }
     }
   }
@@ -811,14 +828,23 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.off_feat = off; off += EPW * g.feat_env_bytes;
   g.off_pos = off; off += EPW * 64 * 8;
   g.off_rew = off; off += EPW * g.rew_env_bytes;
-  // the fast observation path's staging image: 32 rows + 16 bytes of alignment slack
+  // the fast observation path's staging images (one env's rows + 16 bytes of alignment
+  // slack each) for a group of 64 lanes (the whole wave) or 32 (each half in turn),
+  // aliasing dep onwards; the whole wave while the block stays within 40 KB (4 blocks
+  // per CU)
   g.off_stage = -1;
-  g.stage_env_bytes = round_up(std::min(L, 32) * g.D * 4 + 16, 16);
+  g.stage_lanes = 0;
+  g.stage_env_bytes = round_up(L * g.D * 4 + 16, 16);
   if (g.K == 5 && (g.win == 3 || g.win == 5 || g.win == 7) && L >= 8 && L <= 32) {
-    const int st = (32 / std::min(L, 32)) * g.stage_env_bytes;
-    if (off + st <= 64 * 1024) {
-      g.off_stage = off;
-      off += st;
+    for (int G : {64, 32}) {
+      const int st = std::min(EPW, G / L) * g.stage_env_bytes;
+      const int need = std::max(off, g.off_dep + st);
+      if (need <= (G == 64 ? 40 * 1024 : 64 * 1024)) {
+        g.off_stage = g.off_dep;
+        g.stage_lanes = G;
+        off = need;
+        break;
+      }
     }
   }
   g.lds = off;

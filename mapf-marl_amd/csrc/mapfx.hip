@@ -1367,6 +1367,16 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
 //   D  step s's neighbour bytes, dones, t and all-done ballot  (dependency chain)
 // so only A and D (a few dozen instructions) sit on the serial chain between
 // steps.  The last step's heavy part and tails run after the loop.
+// Wave priorities of the split (s_setprio): the store wave's per-step chain is the
+// longer one (the step wave waits for it at the hand-over barrier), so it wins issue
+// arbitration against the other blocks' waves on its SIMD.  C2: -3 % (T = 20) to
+// -6 % (T = 64) kernel time; raising the step wave instead measured neutral.
+#ifndef MAPFX_PRIO_STEP
+#define MAPFX_PRIO_STEP 0
+#endif
+#ifndef MAPFX_PRIO_STORE
+#define MAPFX_PRIO_STORE 3
+#endif
 template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false>
 __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g0) {
   Args a = a0;
@@ -1376,6 +1386,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   static_assert(!SPLIT || (ROLL && FULLW && RUNNER && LL == 16 && WIN > 0), "split: runner rollout, N = 16");
   if constexpr (SPLIT) {
     if (threadIdx.x >= 64) {  // the output side of the split
+      if (MAPFX_PRIO_STORE) __builtin_amdgcn_s_setprio(MAPFX_PRIO_STORE);
       const int e0 = xcd_block(blockIdx.x, g.nblk) * (64 / LL);
       unsigned char* sp = lds + g.wv_off_split;
       unsigned char* own = sp + 2 * g.wv_split_buf;
@@ -1384,6 +1395,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
       else split_store_wave<WIN, LL, ROLE_SMALL>(g, a, sp, own, e0, threadIdx.x & 63);
       return;
     }
+    if (MAPFX_PRIO_STEP) __builtin_amdgcn_s_setprio(MAPFX_PRIO_STEP);
   }
   constexpr int WW = WIN * WIN;
   constexpr int H2 = WIN / 2;

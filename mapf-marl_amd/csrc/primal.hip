@@ -8,17 +8,19 @@
 // _listNextValidActions (:639-667), on_goal and valid.  Calls are sequential: a
 // later call sees the moves of the earlier ones.
 //
-// One wavefront per world.  The world lives in LDS as an occupant map (0 empty,
-// id + 1) and an obstacle bitmap; for each call lane 0 resolves the move (the
-// only sequential part) and the whole wave builds that agent's 4 x s x s
-// observation (one cell per lane), the visible agents' clamped goals (one agent
-// per lane) and the done ballot.  The goal-vector magnitude comes from a host
+// One lane group of 16, 32 or 64 lanes per world, 64 / lw worlds per wave.  The
+// world lives in LDS as an occupant map (0 empty, id + 1) and an obstacle bitmap;
+// for each call the group's first lane resolves the move (the only sequential
+// part) and the group builds that agent's 4 x s x s observation (one cell per
+// lane), the visible agents' clamped goals (one agent per lane) and the done
+// ballot.  The goal-vector magnitude comes from a host
 // libm pow LUT, as the reference computes `(dx**2 + dy**2) ** .5` (quirk 8).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -36,6 +38,7 @@ struct QGeo {
   int H, W, N, E, s, map_shared;
   long long map_stride;
   int hw, bits_words, lut_n;
+  int lw, lw_shift, wreg;  // lanes per world (16 / 32 / 64), log2, LDS bytes per world
 };
 
 struct QArgs {
@@ -65,170 +68,216 @@ __device__ inline void wave_fence() {
 __device__ inline int dir_r(int a) { return a == 2 ? 1 : (a == 4 ? -1 : 0); }  // dirDict :28
 __device__ inline int dir_c(int a) { return a == 1 ? 1 : (a == 3 ? -1 : 0); }
 
+// One wave holds 64 / lw worlds, lw lanes each (lw = 16, 32 or 64; the host picks it
+// from N and the grid size).  A call is a chain of LDS round trips (move ->
+// post-move reads -> goal stamps -> stores), and the waves are too few to hide
+// them, so the chain is kept short: every LDS read a step needs is issued in one
+// batch (the move's cell and obstacle word, the observation cells of the next
+// step, the next-action probes, the agents), the visible-goals plane is a
+// per-call stamp (no clearing pass), and the next call's (id, action) is read
+// while this one runs.
+constexpr int PR_IT = 4;  // observation cells per lane held in registers (s*s <= 4 lw)
+
 __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
   extern __shared__ __align__(16) unsigned char lds[];
-  const int e = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int N = g.N, H = g.H, W = g.W, s = g.s;
-  uint8_t* occ = lds;                                   // [H*W] 0 empty, id + 1
-  uint32_t* obst = (uint32_t*)(lds + ((g.hw + 15) & ~15));  // [bits_words]
+  const int lw = g.lw, lane = threadIdx.x;
+  const int wl = lane >> g.lw_shift, ag = lane & (lw - 1), lead = wl << g.lw_shift;
+  const int e = blockIdx.x * (64 >> g.lw_shift) + wl;
+  const bool live = e < g.E;
+  const uint64_t wmask = (lw == 64 ? ~0ull : ((1ull << lw) - 1ull)) << lead;
+  const int N = g.N, H = g.H, W = g.W, s = g.s, ss = s * s;
+  unsigned char* wr = lds + wl * g.wreg;
+  uint8_t* occ = wr;                                           // [H*W] 0 empty, id + 1
+  uint32_t* obst = (uint32_t*)(wr + ((g.hw + 15) & ~15));      // [bits_words]
   int2* pos = (int2*)((unsigned char*)obst + ((g.bits_words * 4 + 15) & ~15));  // [N]
-  int2* gl = pos + N;                                   // [N]
-  uint8_t* goals_plane = (uint8_t*)(gl + N);            // [s*s]
-  int* flag = (int*)(goals_plane + ((s * s + 15) & ~15));  // [2]: bad call
+  int2* gl = pos + N;                                          // [N]
+  int2* pend = gl + N;                                         // [64] goal vector (dx, dy) of a block's calls
+  int2* pairL = pend + 64;                                     // [64] a block's (agent id, action)
+  int* flag = (int*)(pairL + 64);                              // [4] move status
+  int* stamp = flag + 4;                                       // [s*s] call k + 1 marks a visible goal
 
-  for (int i = lane; i < g.hw; i += 64) occ[i] = 0;
-  const uint32_t* src = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)e * g.map_stride));
-  for (int w = lane; w < g.bits_words; w += 64) obst[w] = src[w];
-  for (int b = lane; b < N; b += 64) {
-    pos[b] = ((const int2*)a.pos)[(long long)e * N + b];
-    gl[b] = ((const int2*)a.goal)[(long long)e * N + b];
+  if (live) {
+    for (int i = ag; i < g.hw; i += lw) occ[i] = 0;
+    for (int i = ag; i < ss; i += lw) stamp[i] = 0;
+    const uint32_t* src = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)e * g.map_stride));
+    for (int w = ag; w < g.bits_words; w += lw) obst[w] = src[w];
+    for (int b = ag; b < N; b += lw) {
+      pos[b] = ((const int2*)a.pos)[(long long)e * N + b];
+      gl[b] = ((const int2*)a.goal)[(long long)e * N + b];
+    }
   }
   wave_fence();
-  for (int b = lane; b < N; b += 64) occ[pos[b].x * W + pos[b].y] = (uint8_t)(b + 1);
+  if (live)
+    for (int b = ag; b < N; b += lw) occ[pos[b].x * W + pos[b].y] = (uint8_t)(b + 1);
   wave_fence();
-  const auto is_obst = [&](int r, int c) { const int i = r * W + c; return (obst[i >> 5] >> (i & 31)) & 1u; };
+  // this lane's first observation cell (ag / s, ag % s) and the step to its next one
+  const int r_step = lw / s, c_step = lw % s;
+  const int r0 = ag / s, c0 = ag % s;
+  const bool probe = ag >= 1 && ag <= 4;  // lanes 1..4 test the next-action directions
 
-  // the calls' (agent id, action) pairs: lane l holds call 64 b + l of block b, the
-  // next block is loaded while this one runs, and each call reads its pair with
-  // v_readlane (uniform index) -- no HBM round trip inside the sequential loop
   const long long e0k = (long long)e * a.K;
-  int id_c = 0, act_c = 0, id_n = 0, act_n = 0;
-  if (lane < a.K) {
-    id_n = a.ids[e0k + lane];
-    act_n = a.acts[e0k + lane];
-  }
-  int pend_dx = 0, pend_dy = 0;
-  const auto flush_vec = [&](int kb, int n) {  // calls kb .. kb + n - 1, one per lane
-    if (lane < n) {
-      const long long ekl = e0k + kb + lane;
-      const double mag = a.pow_lut[pend_dx * pend_dx + pend_dy * pend_dy];
-      double vx = (double)pend_dx, vy = (double)pend_dy;
-      if (mag != 0.0) {
-        vx = vx / mag;
-        vy = vy / mag;
+  int kstop = live ? a.K : 0;  // calls of this world from kstop on are not run (bad call)
+  for (int kb = 0; kb < a.K; kb += 64) {
+    const int kend = min(a.K, kb + 64);
+    // the block's (id, action) pairs -> LDS: one load wait per 64 calls (on gfx9
+    // vmcnt also counts stores, so a wait drains the earlier calls' outputs)
+    if (kb < kstop)
+      for (int j = ag; j < kend - kb; j += lw) pairL[j] = make_int2(a.ids[e0k + kb + j], a.acts[e0k + kb + j]);
+    wave_fence();
+    int2 pa = pairL[0];
+    for (int k = kb; k < kend; ++k) {
+      const int2 nxt = pairL[min(k + 1 - kb, 63)];  // the next call's pair, read ahead
+      const int aid = pa.x - 1, act = pa.y;
+      pa = nxt;
+      if (k >= kstop) continue;  // (uniform within a world)
+      const long long ek = e0k + k;
+      if (aid < 0 || aid >= N || act < 0 || act > 4) {  // the reference asserts (:556-558)
+        if (ag == 0 && a.err) atomicCAS(a.err, 0, e + 1);
+        kstop = k;
+        continue;
       }
-      a.vec[ekl * 3 + 0] = vx;
-      a.vec[ekl * 3 + 1] = vy;
-      a.vec[ekl * 3 + 2] = mag;
-    }
-  };
-  for (int k = 0; k < a.K; ++k) {
-    const long long ek = e0k + k;
-    if ((k & 63) == 0) {
-      id_c = id_n;
-      act_c = act_n;
-      if (k + 64 + lane < a.K) {
-        id_n = a.ids[ek + 64 + lane];
-        act_n = a.acts[ek + 64 + lane];
-      }
-    }
-    const int aid = __builtin_amdgcn_readlane(id_c, k & 63) - 1;
-    const int act = __builtin_amdgcn_readlane(act_c, k & 63);
-    if (aid < 0 || aid >= N || act < 0 || act > 4) {  // the reference asserts (:556-558)
-      if (lane == 0 && a.err) atomicCAS(a.err, 0, e + 1);
-      if (a.vec && (k & 63)) flush_vec(k & ~63, k & 63);  // the block's earlier calls
-      break;
-    }
-    // ---- State.moveAgent (:103-135), lane 0 ----
-    int status = 0;
-    if (lane == 0) {
-      const int ax = pos[aid].x, ay = pos[aid].y;
-      const int2 gg = gl[aid];
-      if (act == 0) {
-        status = (gg.x == ax && gg.y == ay) ? 1 : 0;
-      } else {
-        const int nx = ax + dir_r(act), ny = ay + dir_c(act);
-        if (nx >= H || nx < 0 || ny >= W || ny < 0) status = -1;
-        else if (occ[nx * W + ny] != 0) status = -3;   // state > 0 (agents own their cell)
-        else if (is_obst(nx, ny)) status = -2;
+      // ---- State.moveAgent (:103-135), the world's first lane ----
+      if (ag == 0) {
+        const int2 p = pos[aid], gg = gl[aid];
+        const int nx = p.x + dir_r(act), ny = p.y + dir_c(act);
+        const bool inb = nx < H && nx >= 0 && ny < W && ny >= 0;
+        const int ci = inb ? nx * W + ny : 0;
+        const uint8_t oc = occ[ci];
+        const uint32_t ow = obst[ci >> 5];
+        int status;
+        if (act == 0) status = (gg.x == p.x && gg.y == p.y) ? 1 : 0;
+        else if (!inb) status = -1;
+        else if (oc != 0) status = -3;                 // state > 0 (agents own their cell)
+        else if ((ow >> (ci & 31)) & 1u) status = -2;
         else {
-          occ[ax * W + ay] = 0;
-          occ[nx * W + ny] = (uint8_t)(aid + 1);
+          occ[p.x * W + p.y] = 0;
+          occ[ci] = (uint8_t)(aid + 1);
           pos[aid] = make_int2(nx, ny);
           if (gg.x == nx && gg.y == ny) status = 1;
-          else if (gg.x == ax && gg.y == ay) status = 2;
+          else if (gg.x == p.x && gg.y == p.y) status = 2;
           else status = 0;
         }
-      }
-      flag[0] = status;
-    }
-    wave_fence();
-    status = flag[0];
-    const int ax = pos[aid].x, ay = pos[aid].y;
-    const int2 gg = gl[aid];
-    // ---- done: every agent on its goal (:159-166) ----
-    bool off = false;
-    for (int b = lane; b < N; b += 64) off |= (pos[b].x != gl[b].x) || (pos[b].y != gl[b].y);
-    const bool done = __ballot(off) == 0;
-    // ---- _observe (:343-386) ----
-    const int tr = ax - s / 2, tc = ay - s / 2;
-    if (a.obs) {
-      for (int i = lane; i < s * s; i += 64) goals_plane[i] = 0;
-      wave_fence();
-      for (int b = lane; b < N; b += 64) {  // visible agents' goals, clamped into view (:374-378)
-        if (b == aid) continue;
-        const int br = pos[b].x, bc = pos[b].y;
-        if (br >= tr && br < tr + s && bc >= tc && bc < tc + s) {
-          const int mr = max(tr, min(tr + s - 1, gl[b].x));
-          const int mc = max(tc, min(tc + s - 1, gl[b].y));
-          goals_plane[(mr - tr) * s + (mc - tc)] = 1;
-        }
+        flag[0] = status;
       }
       wave_fence();
-      uint8_t* o = a.obs + ek * 4 * s * s;
-      for (int i = lane; i < s * s; i += 64) {
-        const int r = tr + i / s, c = tc + i % s;
-        uint8_t poss = 0, goal = 0, ob = 0;
-        if (r >= H || r < 0 || c >= W || c < 0) {
-          ob = 1;  // :356-359
-        } else {
-          const bool agent = occ[r * W + c] != 0;
-          if (!agent && is_obst(r, c)) ob = 1;    // :360-362
-          if (agent) poss = 1;                    // :363-365, 369-372
-          if (r == gg.x && c == gg.y) goal = 1;   // :366-368
+      // ---- one batch of LDS reads on the post-move world ----
+      const int status = flag[0];
+      const int2 p = pos[aid], gg = gl[aid];
+      const int ax = p.x, ay = p.y;
+      const int tr = ax - s / 2, tc = ay - s / 2;
+      // _observe cells (:343-386) held in registers: occupant and obstacle word
+      uint8_t ocv[PR_IT];
+      uint32_t obv[PR_IT];
+      int cidx[PR_IT];  // map cell, -1 outside the map
+      {
+        int rr = r0, cc = c0;
+#pragma unroll
+        for (int it = 0; it < PR_IT; ++it) {
+          const int r = tr + rr, c = tc + cc;
+          const bool in = ag + it * lw < ss && r < H && r >= 0 && c < W && c >= 0;
+          cidx[it] = in ? r * W + c : -1;
+          const int ci = in ? r * W + c : 0;
+          ocv[it] = a.obs ? occ[ci] : 0;
+          obv[it] = a.obs ? obst[ci >> 5] : 0;
+          rr += r_step;
+          cc += c_step;
+          if (cc >= s) {
+            cc -= s;
+            ++rr;
+          }
         }
-        o[i] = poss;
-        o[s * s + i] = goal;
-        o[2 * s * s + i] = goals_plane[i];
-        o[3 * s * s + i] = ob;
+      }
+      // _listNextValidActions (:639-667): direction ag probed by lane ag of the world
+      bool ok = false;
+      if (probe) {
+        const int nx = ax + dir_r(ag), ny = ay + dir_c(ag);
+        const bool inb = nx < H && nx >= 0 && ny < W && ny >= 0;
+        const int ci = inb ? nx * W + ny : 0;
+        ok = inb && occ[ci] == 0 && !((obst[ci >> 5] >> (ci & 31)) & 1u);
+      }
+      // agents: done (:159-166) and visible agents' goals, clamped into view (:374-378)
+      bool off = false;
+      for (int b = ag; b < N; b += lw) {
+        const int2 pb = pos[b], gb = gl[b];
+        off |= (pb.x != gb.x) || (pb.y != gb.y);
+        if (a.obs && b != aid && pb.x >= tr && pb.x < tr + s && pb.y >= tc && pb.y < tc + s) {
+          const int mr = max(tr, min(tr + s - 1, gb.x));
+          const int mc = max(tc, min(tc + s - 1, gb.y));
+          stamp[(mr - tr) * s + (mc - tc)] = k + 1;
+        }
+      }
+      const bool done = (__ballot(off) & wmask) == 0;
+      const uint32_t mbits = (uint32_t)(__ballot(ok) >> lead) & 0x1Eu;  // bits 1..4 = actions
+      wave_fence();
+      if (a.obs) {
+        uint8_t* o = a.obs + ek * 4 * ss;
+        const auto cell = [&](int i, int ci, uint8_t oc, uint32_t ow) {
+          uint8_t poss = 0, goal = 0, ob = 1;  // outside the map: obstacle (:356-359)
+          if (ci >= 0) {
+            const bool agent = oc != 0;
+            ob = (!agent && ((ow >> (ci & 31)) & 1u)) ? 1 : 0;  // :360-362
+            poss = agent ? 1 : 0;                                // :363-365, 369-372
+            goal = (ci == gg.x * W + gg.y) ? 1 : 0;               // :366-368
+          }
+          o[i] = poss;
+          o[ss + i] = goal;
+          o[2 * ss + i] = stamp[i] == k + 1 ? 1 : 0;
+          o[3 * ss + i] = ob;
+        };
+#pragma unroll
+        for (int it = 0; it < PR_IT; ++it) {
+          const int i = ag + it * lw;
+          if (i < ss) cell(i, cidx[it], ocv[it], obv[it]);
+        }
+        for (int i = ag + PR_IT * lw; i < ss; i += lw) {  // large windows: the rest
+          const int r = tr + i / s, c = tc + i % s;
+          const bool in = r < H && r >= 0 && c < W && c >= 0;
+          const int ci = in ? r * W + c : 0;
+          cell(i, in ? ci : -1, occ[ci], obst[ci >> 5]);
+        }
+      }
+      if (ag == 0) {
+        // ---- reward (:579-596), JOINT = False; stay-on-goal blocking term = 0 ----
+        double rew;
+        if (act == 0) rew = status == 1 ? GOAL_REWARD + 0 : IDLE_COST;
+        else if (status == 1) rew = GOAL_REWARD;
+        else if (status < 0) rew = COLLISION_REWARD;
+        else rew = ACTION_COST;
+        uint32_t m = 1u | mbits;
+        const int opp = act == 1 ? 3 : act == 2 ? 4 : act == 3 ? 1 : act == 4 ? 2 : -1;  // :26
+        if (opp > 0) m &= ~(1u << opp);
+        if (a.reward) a.reward[ek] = rew;
+        if (a.done) a.done[ek] = done ? 1 : 0;
+        if (a.next_mask) a.next_mask[ek] = (uint8_t)m;
+        if (a.on_goal) a.on_goal[ek] = (ax == gg.x && ay == gg.y) ? 1 : 0;
+        if (a.valid) a.valid[ek] = status >= 0 ? 1 : 0;
+        // goal vector (:379-384): its magnitude needs a LUT load, so the call's
+        // (dx, dy) waits in LDS and the world writes a block's vectors together
+        // (one load latency per 64 calls instead of one per call)
+        pend[k - kb] = make_int2(gg.x - ax, gg.y - ay);
+      }
+      wave_fence();
+    }
+    if (a.vec) {  // the block's goal vectors, calls kb .. min(kend, kstop) - 1
+      const int n = min(kend, kstop) - kb;
+      for (int j = ag; j < n; j += lw) {
+        const int2 d = pend[j];
+        const double mag = a.pow_lut[d.x * d.x + d.y * d.y];
+        double vx = (double)d.x, vy = (double)d.y;
+        if (mag != 0.0) {
+          vx = vx / mag;
+          vy = vy / mag;
+        }
+        double* v = a.vec + (e0k + kb + j) * 3;
+        v[0] = vx;
+        v[1] = vy;
+        v[2] = mag;
       }
     }
-    if (lane == 0) {
-      // ---- reward (:579-596), JOINT = False; stay-on-goal blocking term = 0 ----
-      double rew;
-      if (act == 0) rew = status == 1 ? GOAL_REWARD + 0 : IDLE_COST;
-      else if (status == 1) rew = GOAL_REWARD;
-      else if (status < 0) rew = COLLISION_REWARD;
-      else rew = ACTION_COST;
-      // ---- _listNextValidActions (:639-667) ----
-      uint32_t m = 1u;
-      for (int b = 1; b <= 4; ++b) {
-        const int nx = ax + dir_r(b), ny = ay + dir_c(b);
-        if (nx >= H || nx < 0 || ny >= W || ny < 0) continue;
-        if (occ[nx * W + ny] != 0 || is_obst(nx, ny)) continue;
-        m |= 1u << b;
-      }
-      const int opp = act == 1 ? 3 : act == 2 ? 4 : act == 3 ? 1 : act == 4 ? 2 : -1;  // :26
-      if (opp > 0) m &= ~(1u << opp);
-      if (a.reward) a.reward[ek] = rew;
-      if (a.done) a.done[ek] = done ? 1 : 0;
-      if (a.next_mask) a.next_mask[ek] = (uint8_t)m;
-      if (a.on_goal) a.on_goal[ek] = (ax == gg.x && ay == gg.y) ? 1 : 0;
-      if (a.valid) a.valid[ek] = status >= 0 ? 1 : 0;
-    }
-    // goal vector (:379-384): its magnitude needs a LUT load, so lane k & 63 keeps the
-    // call's (dx, dy) and the wave writes a block's 64 vectors together (one load
-    // latency per 64 calls instead of one per call on the sequential path)
-    if (lane == (k & 63)) {
-      pend_dx = gg.x - ax;
-      pend_dy = gg.y - ay;
-    }
-    if (a.vec && ((k & 63) == 63 || k + 1 == a.K)) flush_vec(k & ~63, (k & 63) + 1);
     wave_fence();
   }
-  wave_fence();
-  for (int b = lane; b < N; b += 64) ((int2*)a.pos)[(long long)e * N + b] = pos[b];
+  if (live)
+    for (int b = ag; b < N; b += lw) ((int2*)a.pos)[(long long)e * N + b] = pos[b];
 }
 
 int perr(int code, const char* msg) { return mapfx_internal_error(code, msg); }
@@ -274,8 +323,24 @@ int mapfx_primal_create(const mapfx_primal_cfg* cfg, mapfx_primal_t** out) {
   g.hw = c.H * c.W;
   g.bits_words = (g.hw + 31) / 32;
   g.lut_n = (c.H - 1) * (c.H - 1) + (c.W - 1) * (c.W - 1) + 1;
-  h->lds = ((g.hw + 15) & ~15) + ((g.bits_words * 4 + 15) & ~15) + 16 * g.N +
-           ((g.s * g.s + 15) & ~15) + 16;
+  g.wreg = ((g.hw + 15) & ~15) + ((g.bits_words * 4 + 15) & ~15) + 16 * g.N + 64 * 8 + 64 * 8 + 16 +
+           ((4 * g.s * g.s + 15) & ~15);
+  // Lanes per world: the smallest of 16 / 32 / 64 that covers N, widened while the
+  // grid has fewer than 2 waves per SIMD (2048 waves) or the wave's worlds would
+  // pass 64 KB of LDS.  Packing worlds saves issue slots (the per-call work is
+  // mostly per world, not per cell), more waves hide the call's LDS chain; at
+  // 4096 worlds of N = 16 (the bench) 16 / 32 / 64 lanes measured 190 / 148 / 163 us
+  // per 64-call launch.
+  // MAPFX_PRIMAL_LANES (16 / 32 / 64) overrides the first two rules (tests).
+  g.lw_shift = g.N <= 16 ? 4 : g.N <= 32 ? 5 : 6;
+  const char* force = getenv("MAPFX_PRIMAL_LANES");
+  const int fl = force ? atoi(force) : 0;
+  if (fl == 16 || fl == 32 || fl == 64) g.lw_shift = std::max(g.lw_shift, fl == 16 ? 4 : fl == 32 ? 5 : 6);
+  else
+    while (g.lw_shift < 6 && (long long)(g.E + (64 >> g.lw_shift) - 1) / (64 >> g.lw_shift) < 2048) ++g.lw_shift;
+  while (g.lw_shift < 6 && (64 >> g.lw_shift) * g.wreg > 65536) ++g.lw_shift;
+  g.lw = 1 << g.lw_shift;
+  h->lds = (64 >> g.lw_shift) * g.wreg;
   double* lut = (double*)malloc(sizeof(double) * g.lut_n);
   if (!lut) {
     delete h;
@@ -327,7 +392,8 @@ int mapfx_primal_act(mapfx_primal_t* h, const mapfx_primal_state* st, const int3
     a.vec = out->vec;
     a.err = out->err;
   }
-  hipLaunchKernelGGL(primal_act_kernel, dim3(h->geo.E), dim3(64), h->lds, (hipStream_t)stream,
+  const int wpw = 64 >> h->geo.lw_shift;
+  hipLaunchKernelGGL(primal_act_kernel, dim3((h->geo.E + wpw - 1) / wpw), dim3(64), h->lds, (hipStream_t)stream,
                      h->geo, a);
   return check_hip(hipGetLastError(), "primal_act_kernel launch");
 }

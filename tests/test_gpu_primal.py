@@ -95,14 +95,17 @@ def _random_worlds(rng, E, H, W, N, density, shared):
     return grids, starts, goals
 
 
+@pytest.mark.parametrize("lanes", ["", "16"])  # host's choice (64 at E = 64) / packed lane groups
 @pytest.mark.parametrize("H,W,N,s,K,shared,density", [
     (12, 12, 10, 7, 60, False, 0.2),
     (9, 13, 30, 4, 90, True, 0.1),      # crowded, even window, non-square
     (40, 33, 100, 11, 150, False, 0.15),  # N > 64 (agent loops), s*s > 64
-    (128, 128, 255, 32, 40, True, 0.1),   # the ABI limits: N 255, H*W 16384, s 32
+    (128, 128, 255, 32, 40, True, 0.1),   # the ABI limits: N 255, H*W 16384, s 32 (s*s > 4 * 64: the rest loop)
+    (20, 20, 12, 9, 70, False, 0.1),      # 16-lane groups: s*s = 81 > 4 * 16 (the rest loop)
 ])
-def test_primal_batch_matches_oracle(mapfx_mod, H, W, N, s, K, shared, density):
+def test_primal_batch_matches_oracle(mapfx_mod, monkeypatch, lanes, H, W, N, s, K, shared, density):
     from oracle.primal_dyn_oracle import PrimalWorld
+    monkeypatch.setenv("MAPFX_PRIMAL_LANES", lanes)
     rng = np.random.default_rng(H * 1000 + N)
     E = 64
     grids, starts, goals = _random_worlds(rng, E, H, W, N, density, shared)
@@ -116,6 +119,36 @@ def test_primal_batch_matches_oracle(mapfx_mod, H, W, N, s, K, shared, density):
     for e in list(range(0, E, 16)) + [E - 1]:
         w = PrimalWorld(grids[0 if shared else e], starts[e], goals[e], s)
         for k in range(K):
+            maps, vec, r, done, mask, on_goal, _, valid = w.step(int(ids[e, k]) - 1, int(acts[e, k]))
+            assert np.float64(r).view(np.uint64) == o["reward"][e, k].view(np.uint64), (e, k)
+            assert done == bool(o["done"][e, k]) and mask == int(o["next_mask"][e, k]), (e, k)
+            assert on_goal == bool(o["on_goal"][e, k]) and valid == bool(o["valid"][e, k]), (e, k)
+            assert np.array_equal(maps, o["obs"][e, k]), (e, k)
+            assert np.array_equal(vec.view(np.uint64), o["vec"][e, k].view(np.uint64)), (e, k)
+        assert np.array_equal(np.array(w.pos), pos[e]), e
+
+
+@pytest.mark.parametrize("N", [3, 20, 40])  # 16, 32 and 64 lanes per world (forced)
+def test_primal_bad_call_stops_only_its_world(mapfx_mod, monkeypatch, N):
+    """Worlds share a wave in lane groups: E not a multiple of the worlds per wave,
+    K past one 64-call block, and a bad call in world 2 that ends that world's
+    calls (the reference asserts) while its wave neighbours run on."""
+    from oracle.primal_dyn_oracle import PrimalWorld
+    rng = np.random.default_rng(N)
+    E, H, W, s, K, kbad = 7, 14, 11, 5, 80, 70
+    grids, starts, goals = _random_worlds(rng, E, H, W, N, 0.1, False)
+    ids = rng.integers(1, N + 1, size=(E, K)).astype(np.int32)
+    acts = rng.integers(0, 5, size=(E, K)).astype(np.int32)
+    ids[2, kbad] = N + 1
+    monkeypatch.setenv("MAPFX_PRIMAL_LANES", "16")
+    b = mapfx_mod.PrimalBatch(starts, goals, grids=grids, observation_size=s)
+    o = {k: _np(v).copy() for k, v in b.act(ids, acts).items()}
+    with pytest.raises(AssertionError, match="world 2"):
+        b.check_err()
+    pos = _np(b.pos)
+    for e in range(E):
+        w = PrimalWorld(grids[e], starts[e], goals[e], s)
+        for k in range(kbad if e == 2 else K):
             maps, vec, r, done, mask, on_goal, _, valid = w.step(int(ids[e, k]) - 1, int(acts[e, k]))
             assert np.float64(r).view(np.uint64) == o["reward"][e, k].view(np.uint64), (e, k)
             assert done == bool(o["done"][e, k]) and mask == int(o["next_mask"][e, k]), (e, k)

@@ -177,8 +177,8 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
           const bool in = ag + it * lw < ss && r < H && r >= 0 && c < W && c >= 0;
           cidx[it] = in ? r * W + c : -1;
           const int ci = in ? r * W + c : 0;
-          ocv[it] = a.obs ? occ[ci] : 0;
-          obv[it] = a.obs ? obst[ci >> 5] : 0;
+          ocv[it] = occ[ci];  // (unconditional: cell 0 when outside or no obs)
+          obv[it] = obst[ci >> 5];
           rr += r_step;
           cc += c_step;
           if (cc >= s) {
@@ -211,18 +211,14 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
       wave_fence();
       if (a.obs) {
         uint8_t* o = a.obs + ek * 4 * ss;
-        const auto cell = [&](int i, int ci, uint8_t oc, uint32_t ow) {
-          uint8_t poss = 0, goal = 0, ob = 1;  // outside the map: obstacle (:356-359)
-          if (ci >= 0) {
-            const bool agent = oc != 0;
-            ob = (!agent && ((ow >> (ci & 31)) & 1u)) ? 1 : 0;  // :360-362
-            poss = agent ? 1 : 0;                                // :363-365, 369-372
-            goal = (ci == gg.x * W + gg.y) ? 1 : 0;               // :366-368
-          }
-          o[i] = poss;
-          o[ss + i] = goal;
+        const int gcell = gg.x * W + gg.y;
+        const auto cell = [&](int i, int ci, uint8_t oc, uint32_t ow) {  // branch-free selects
+          const bool in = ci >= 0, agent = oc != 0;
+          const bool wall = ((ow >> (ci & 31)) & 1u) != 0;
+          o[i] = (in && agent) ? 1 : 0;                   // :363-365, 369-372
+          o[ss + i] = ci == gcell ? 1 : 0;                // :366-368 (ci = -1 outside)
           o[2 * ss + i] = stamp[i] == k + 1 ? 1 : 0;
-          o[3 * ss + i] = ob;
+          o[3 * ss + i] = (!in || (!agent && wall)) ? 1 : 0;  // outside: obstacle (:356-362)
         };
 #pragma unroll
         for (int it = 0; it < PR_IT; ++it) {

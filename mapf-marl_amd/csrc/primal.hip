@@ -144,18 +144,17 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
         const int ci = inb ? nx * W + ny : 0;
         const uint8_t oc = occ[ci];
         const uint32_t ow = obst[ci >> 5];
-        int status;
-        if (act == 0) status = (gg.x == p.x && gg.y == p.y) ? 1 : 0;
-        else if (!inb) status = -1;
-        else if (oc != 0) status = -3;                 // state > 0 (agents own their cell)
-        else if ((ow >> (ci & 31)) & 1u) status = -2;
-        else {
+        // the status chain as selects (one branch, for the move's writes)
+        const bool on_old = gg.x == p.x && gg.y == p.y, on_new = gg.x == nx && gg.y == ny;
+        const bool wall = ((ow >> (ci & 31)) & 1u) != 0;
+        const bool moved = act != 0 && inb && oc == 0 && !wall;
+        const int st_move = on_new ? 1 : (on_old ? 2 : 0);
+        const int st_blocked = !inb ? -1 : (oc != 0 ? -3 : -2);  // robot before wall: state > 0
+        const int status = act == 0 ? (on_old ? 1 : 0) : (moved ? st_move : st_blocked);
+        if (moved) {
           occ[p.x * W + p.y] = 0;
           occ[ci] = (uint8_t)(aid + 1);
           pos[aid] = make_int2(nx, ny);
-          if (gg.x == nx && gg.y == ny) status = 1;
-          else if (gg.x == p.x && gg.y == p.y) status = 2;
-          else status = 0;
         }
         flag[0] = status;
       }
@@ -234,11 +233,8 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
       }
       if (ag == 0) {
         // ---- reward (:579-596), JOINT = False; stay-on-goal blocking term = 0 ----
-        double rew;
-        if (act == 0) rew = status == 1 ? GOAL_REWARD + 0 : IDLE_COST;
-        else if (status == 1) rew = GOAL_REWARD;
-        else if (status < 0) rew = COLLISION_REWARD;
-        else rew = ACTION_COST;
+        const double rew = act == 0 ? (status == 1 ? GOAL_REWARD + 0 : IDLE_COST)
+                                    : status == 1 ? GOAL_REWARD : status < 0 ? COLLISION_REWARD : ACTION_COST;
         uint32_t m = 1u | mbits;
         const int opp = act == 1 ? 3 : act == 2 ? 4 : act == 3 ? 1 : act == 4 ? 2 : -1;  // :26
         if (opp > 0) m &= ~(1u << opp);

@@ -78,14 +78,19 @@ __device__ inline int dir_c(int a) { return a == 1 ? 1 : (a == 3 ? -1 : 0); }
 // while this one runs.
 constexpr int PR_IT = 4;  // observation cells per lane held in registers (s*s <= 4 lw)
 
+// S, LS: observation size and log2(lanes per world) fixed at compile time (0: from
+// QGeo).  PRIMAL's default observation_size (10, `:175`) gets specialised kernels:
+// the window walk and the planes' store offsets become immediates.
+template <int S, int LS>
 __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
   extern __shared__ __align__(16) unsigned char lds[];
-  const int lw = g.lw, lane = threadIdx.x;
-  const int wl = lane >> g.lw_shift, ag = lane & (lw - 1), lead = wl << g.lw_shift;
-  const int e = blockIdx.x * (64 >> g.lw_shift) + wl;
+  const int lws = LS ? LS : g.lw_shift;
+  const int lw = 1 << lws, lane = threadIdx.x;
+  const int wl = lane >> lws, ag = lane & (lw - 1), lead = wl << lws;
+  const int e = blockIdx.x * (64 >> lws) + wl;
   const bool live = e < g.E;
   const uint64_t wmask = (lw == 64 ? ~0ull : ((1ull << lw) - 1ull)) << lead;
-  const int N = g.N, H = g.H, W = g.W, s = g.s, ss = s * s;
+  const int N = g.N, H = g.H, W = g.W, s = S ? S : g.s, ss = s * s;
   unsigned char* wr = lds + wl * g.wreg;
   uint8_t* occ = wr;                                           // [H*W] 0 empty, id + 1
   uint32_t* obst = (uint32_t*)(wr + ((g.hw + 15) & ~15));      // [bits_words]
@@ -385,8 +390,13 @@ int mapfx_primal_act(mapfx_primal_t* h, const mapfx_primal_state* st, const int3
     a.err = out->err;
   }
   const int wpw = 64 >> h->geo.lw_shift;
-  hipLaunchKernelGGL(primal_act_kernel, dim3((h->geo.E + wpw - 1) / wpw), dim3(64), h->lds, (hipStream_t)stream,
-                     h->geo, a);
+  const dim3 grid((h->geo.E + wpw - 1) / wpw), block(64);
+  const hipStream_t sm = (hipStream_t)stream;
+  const QGeo& g = h->geo;
+  if (g.s == 10 && g.lw_shift == 4) hipLaunchKernelGGL((primal_act_kernel<10, 4>), grid, block, h->lds, sm, g, a);
+  else if (g.s == 10 && g.lw_shift == 5) hipLaunchKernelGGL((primal_act_kernel<10, 5>), grid, block, h->lds, sm, g, a);
+  else if (g.s == 10 && g.lw_shift == 6) hipLaunchKernelGGL((primal_act_kernel<10, 6>), grid, block, h->lds, sm, g, a);
+  else hipLaunchKernelGGL((primal_act_kernel<0, 0>), grid, block, h->lds, sm, g, a);
   return check_hip(hipGetLastError(), "primal_act_kernel launch");
 }
 

@@ -95,13 +95,15 @@ def _random_worlds(rng, E, H, W, N, density, shared):
     return grids, starts, goals
 
 
-@pytest.mark.parametrize("lanes", ["", "16"])  # host's choice (64 at E = 64) / packed lane groups
+@pytest.mark.parametrize("lanes", ["", "16", "32"])  # host's choice (64 at E = 64) / packed lane groups
 @pytest.mark.parametrize("H,W,N,s,K,shared,density", [
     (12, 12, 10, 7, 60, False, 0.2),
     (9, 13, 30, 4, 90, True, 0.1),      # crowded, even window, non-square
     (40, 33, 100, 11, 150, False, 0.15),  # N > 64 (agent loops), s*s > 64
     (128, 128, 255, 32, 40, True, 0.1),   # the ABI limits: N 255, H*W 16384, s 32 (s*s > 4 * 64: the rest loop)
     (20, 20, 12, 9, 70, False, 0.1),      # 16-lane groups: s*s = 81 > 4 * 16 (the rest loop)
+    (32, 32, 16, 10, 70, False, 0.1),     # observation_size 10 (the default): specialised kernels
+    (15, 17, 40, 10, 66, True, 0.1),      # s = 10 at 64 lanes (N > 32)
 ])
 def test_primal_batch_matches_oracle(mapfx_mod, monkeypatch, lanes, H, W, N, s, K, shared, density):
     from oracle.primal_dyn_oracle import PrimalWorld

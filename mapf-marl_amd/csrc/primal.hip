@@ -326,7 +326,7 @@ int mapfx_primal_create(const mapfx_primal_cfg* cfg, mapfx_primal_t** out) {
   // grid has fewer than 2 waves per SIMD (2048 waves) or the wave's worlds would
   // pass 64 KB of LDS.  Packing worlds saves issue slots (the per-call work is
   // mostly per world, not per cell), more waves hide the call's LDS chain; at
-  // 4096 worlds of N = 16 (the bench) 16 / 32 / 64 lanes measured 190 / 148 / 163 us
+  // 4096 worlds of N = 16 (the bench) 16 / 32 / 64 lanes measured 149 / 120 / 125 us
   // per 64-call launch.
   // MAPFX_PRIMAL_LANES (16 / 32 / 64) overrides the first two rules (tests).
   g.lw_shift = g.N <= 16 ? 4 : g.N <= 32 ? 5 : 6;

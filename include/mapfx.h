@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MAPFX_ABI_VERSION 2
+#define MAPFX_ABI_VERSION 3
 
 /* error codes */
 #define MAPFX_OK 0
@@ -93,7 +93,8 @@ typedef struct mapfx_out {
   float* reward_f32;     /* [E]  same value rounded to fp32                      */
   uint8_t* term;         /* [E]  1 iff every agent is done (episode_done)        */
   uint8_t* node;         /* [E][N] node-collision flag (0/1)                     */
-  uint8_t* edge;         /* [E][N] edge-collision count (saturates at 255)       */
+  uint8_t* edge;         /* [E][N] edge-collision count, exact: u8 for N <= 256,
+                            u16 above (mapfx_edge_elem_size; ABI 3)              */
   uint8_t* avail;        /* [E][N] 5-bit mask, bit d = action d available        */
   void* obs_full;        /* [E][H*W] occupancy G + counts                        */
   void* obs_window;      /* [E][N][2][w][w] {obstacle, agents} window            */
@@ -132,6 +133,9 @@ const char* mapfx_last_error(void);
 int64_t mapfx_map_stride(int32_t H, int32_t W);
 /* 1 or 2: element size of obs_full / obs_window for N agents. */
 int32_t mapfx_obs_elem_size(int32_t n_agents);
+/* 1 or 2: element size of `edge` for N agents (an edge count is at most N - 1,
+ * envs/mapf_gridworld.py:364-383, so u8 holds it while N <= 256).  ABI 3. */
+int32_t mapfx_edge_elem_size(int32_t n_agents);
 
 int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle);
 void mapfx_destroy(mapfx_t* h);

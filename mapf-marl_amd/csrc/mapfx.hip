@@ -375,7 +375,7 @@ __device__ void write_occ16_rows(const Geo& g, const unsigned char* lds, const i
       P[j] = (((c & 0x7FFF7FFFu) | 0x80008000u) - ((c >> 15) & 0x00010001u)) ^ 0x80008000u;
     }
     const uint32_t O = 2u * (uint32_t)(q * (W * W) + y * W);
-    if ((O & 2u) == 0) {
+    if ((((uintptr_t)dst + O) & 2u) == 0) {  // parity of the absolute address (dst may be 2 mod 4)
 #pragma unroll
       for (int j = 0; j + 1 < NP; ++j) *(uint32_t*)(dst + O + 4 * j) = P[j];
       *(uint16_t*)(dst + O + 4 * (NP - 1)) = (uint16_t)P[NP - 1];
@@ -601,7 +601,10 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       if (MAPFX_GABL & 4) continue;
       if (a.do_step) {
         if (a.node) a.node[ai] = (uint8_t)node;
-        if (a.edge) a.edge[ai] = (uint8_t)(edge > 255 ? 255 : edge);
+        if (a.edge) {  // u8 while N <= 256 (edge <= N - 1), else u16 (mapfx_edge_elem_size)
+          if (N <= 256) a.edge[ai] = (uint8_t)edge;
+          else ((uint16_t*)a.edge)[ai] = (uint16_t)edge;
+        }
       }
       if (a.traj_pos) ((int2*)a.traj_pos)[ai] = make_int2(r[k], c[k]);
       if (a.traj_done) a.traj_done[ai] = dn[k] ? 1 : 0;
@@ -2163,6 +2166,8 @@ int64_t mapfx_map_stride(int32_t H, int32_t W) {
 }
 
 int32_t mapfx_obs_elem_size(int32_t n_agents) { return n_agents <= 127 ? 1 : 2; }
+
+int32_t mapfx_edge_elem_size(int32_t n_agents) { return n_agents <= 256 ? 1 : 2; }
 
 int32_t mapfx_action(uint64_t seed, int64_t env, int32_t t, int32_t agent) {
   return gen_action(seed, env, t, agent);

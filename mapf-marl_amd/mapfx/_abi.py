@@ -86,6 +86,7 @@ class QOut(ctypes.Structure):
 # every symbol include/mapfx.h, include/mapfx_partial.h and include/mapfx_primal.h declare
 # (checked by tests/test_abi_exports.py)
 EXPORTS = ("mapfx_abi_version", "mapfx_last_error", "mapfx_map_stride", "mapfx_obs_elem_size",
+           "mapfx_edge_elem_size",
            "mapfx_create", "mapfx_destroy", "mapfx_query", "mapfx_reset", "mapfx_step",
            "mapfx_observe", "mapfx_rollout", "mapfx_rollout_timed", "mapfx_gen_actions", "mapfx_action",
            "mapfx_partial_create", "mapfx_partial_destroy", "mapfx_partial_obs_dim",
@@ -107,7 +108,7 @@ class RState(ctypes.Structure):  # include/mapfx_runner.h mapfx_runner_state
                             "env_steps", "env_actions")]
 
 
-ABI_VERSION = 2  # include/mapfx.h MAPFX_ABI_VERSION
+ABI_VERSION = 3  # include/mapfx.h MAPFX_ABI_VERSION
 
 
 class MapfxError(RuntimeError):
@@ -125,6 +126,7 @@ def _load():
         "mapfx_last_error": (ctypes.c_char_p, []),
         "mapfx_map_stride": (c_i64, [c_i32, c_i32]),
         "mapfx_obs_elem_size": (c_i32, [c_i32]),
+        "mapfx_edge_elem_size": (c_i32, [c_i32]),
         "mapfx_create": (c_i32, [P(Cfg), P(c_vp)]),
         "mapfx_destroy": (None, [c_vp]),
         "mapfx_query": (c_i32, [c_vp, P(Info)]),

@@ -95,6 +95,7 @@ class MapfGridBatch:
         self.init_pos = init_pos.to(dev).contiguous()
         self.goal = goals.to(dev).contiguous()
         self.obs_elem = torch.int8 if lib.mapfx_obs_elem_size(self.N) == 1 else torch.int16
+        self.edge_elem = torch.uint8 if lib.mapfx_edge_elem_size(self.N) == 1 else torch.int16  # counts < 2^15
         self.err = torch.zeros((1,), dtype=torch.int32, device=dev)
         # `packed`: the mutable state and every per-step output are views of ONE flat
         # device buffer (mapfx.dist.ChunkLayout), so a host mirror of all of it is a
@@ -123,7 +124,7 @@ class MapfGridBatch:
                 if track_steps else None
             self.out = self._alloc_out(None)
         self._out_cache = {}          # outputs selection -> Out struct over self.out
-        self._traj_cache = {}         # (id(traj), outputs) -> Out struct over a trajectory
+        self._traj_cache = {}         # (outputs, buffer pointers) -> Out struct
         self._dev_index = self.device.index if self.device.index is not None \
             else torch.cuda.current_device()
         self._act_shape = (self.E, self.N)
@@ -142,7 +143,7 @@ class MapfGridBatch:
             "reward_f32": (lead + (E,), torch.float32),
             "term": (lead + (E,), torch.uint8),
             "node": (lead + (E, N), torch.uint8),
-            "edge": (lead + (E, N), torch.uint8),
+            "edge": (lead + (E, N), self.edge_elem),
             "avail": (lead + (E, N), torch.uint8),
         }
         if "full" in self.obs_kinds:
@@ -242,17 +243,19 @@ class MapfGridBatch:
         return self.out
 
     def _traj_struct(self, traj, outputs):
-        """Out struct over a caller's trajectory dict, cached per (dict, outputs):
-        repeated rollouts into the same buffers build no ctypes objects."""
-        k = (id(traj), None if outputs is None else tuple(outputs))
-        hit = self._traj_cache.get(k)
-        if hit is not None and hit[0] is traj and all(
-                hit[1].get(n) is traj.get(n) for n in hit[1]):
-            return hit[2]
-        s = self._out_struct(traj, keys=k[1])
-        if len(self._traj_cache) > 64:
-            self._traj_cache.clear()
-        self._traj_cache[k] = (traj, dict(traj), s)
+        """Out struct over a trajectory dict, cached by the buffers' device pointers:
+        repeated rollouts into the same buffers build no ctypes objects, and the
+        cache holds no reference to any tensor (the struct is pointers only, so an
+        entry keyed by equal pointers is the same struct)."""
+        keys = None if outputs is None else tuple(outputs)
+        k = (keys,) + tuple((n, v.data_ptr()) for n, v in traj.items()
+                            if isinstance(v, torch.Tensor))
+        s = self._traj_cache.get(k)
+        if s is None:
+            s = self._out_struct(traj, keys=keys)
+            if len(self._traj_cache) >= 64:
+                self._traj_cache.clear()
+            self._traj_cache[k] = s
         return s
 
     def _rollout_actions(self, T, actions):

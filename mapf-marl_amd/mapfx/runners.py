@@ -24,7 +24,9 @@ reference ParallelRunner itself), including its stale list: the MAC's `bs` and t
 actions row at step t cover the envs that were running before step t - 1.  The
 MAC gets `bs` as a device LongTensor of length B (ascending running env ids,
 padded with the first one), a form the reference EpisodeBatch / BasicMAC index
-with (episode_buffer.py:186-190).
+with (episode_buffer.py:186-190); `args.runner_exact_bs` passes the exact-length
+list instead (one host sync per step, for stochastic action selectors whose RNG
+consumption must follow the reference's).
 
 Per-env instances: every reset draws each env's scenario like
 MARL_PARTIAL_ENV.__setup_agent (:896-920: random.randint(1, 25) then
@@ -258,6 +260,12 @@ class ParallelRunner:
         sh = stream.cuda_stream
         fixed = (env._h, ctypes.byref(env._state), ctypes.byref(env._out), rs)
         step = lib.mapfx_runner_step
+        # The MAC gets `bs` padded to B (no host sync per step); a stochastic selector
+        # then draws random numbers for B rows, not len(bs) as the reference does
+        # (parallel_runner.py:106), so its RNG stream diverges once an env has
+        # terminated.  args.runner_exact_bs = True passes bs[:len(bs)] instead, at the
+        # cost of one host sync per step (the count of the previous step's compaction).
+        exact_bs = bool(getattr(self.args, "runner_exact_bs", False))
         k = 0
         while True:
             if k >= 2:   # no env running after step k - 2: the reference stopped at k - 1
@@ -265,9 +273,14 @@ class ParallelRunner:
                 ev.synchronize()
                 if int(hc[1]) == 0:
                     break
-            actions = self.mac.select_actions(self.batch, t_ep=k, t_env=self.t_env, bs=self._bs,
+            bs = self._bs
+            if exact_bs and k >= 1:   # len(bs) from step k - 1's compaction (one sync)
+                ev, hc, _ = self._ring[(k - 1) % _RING]
+                ev.synchronize()
+                bs = self._bs[:int(hc[0])]
+            actions = self.mac.select_actions(self.batch, t_ep=k, t_env=self.t_env, bs=bs,
                                               test_mode=test_mode)
-            a = actions.reshape(self.batch_size, self.n_agents)
+            a = actions.reshape(-1, self.n_agents)   # row j is env bs[j] (j < len(bs) read)
             if a.device != self.device:
                 a = a.to(self.device)
             if a.dtype not in _ADT:
@@ -282,6 +295,9 @@ class ParallelRunner:
         self.t = k
         # the run's totals: one transfer at the end
         env_steps = int(self._env_steps.item())
+        # an env given an action outside 0..4 was not stepped (its rows say reward 0):
+        # the reference asserts at marl_partial.py:177
+        env.check_err()
         returns = self._ep_return.cpu().tolist()
         lengths = self._ep_length.cpu()
         self.env_steps_this_run = 0 if test_mode else env_steps

@@ -73,7 +73,7 @@ class OracleBatch:
     def step(self, actions):
         a = np.ascontiguousarray(actions, dtype=np.int32)
         out = {"reward": np.zeros(self.E, np.float64), "node": np.zeros((self.E, self.N), np.uint8),
-               "edge": np.zeros((self.E, self.N), np.uint8)}
+               "edge": np.zeros((self.E, self.N), np.uint16)}
         bad = lib().orc_step(ctypes.byref(self.cfg), _p(self.pos), _p(self.goal), _p(self.done),
                              _p(self.t), _p(self.steps), _p(self.bits), _p(a), _p(out["reward"]),
                              _p(out["node"]), _p(out["edge"]), ctypes.c_int(self.nthreads))
@@ -100,7 +100,7 @@ class OracleBatch:
     def rollout(self, T, seed, t0=0, window=5):
         E, N = self.E, self.N
         out = {"reward": np.zeros(E, np.float64), "node": np.zeros((E, N), np.uint8),
-               "edge": np.zeros((E, N), np.uint8), "avail": np.zeros((E, N), np.uint8),
+               "edge": np.zeros((E, N), np.uint16), "avail": np.zeros((E, N), np.uint8),
                "obs_window": np.zeros((E, N, 2, window, window), self.obs_dt)}
         lib().orc_rollout(ctypes.byref(self.cfg), ctypes.c_int32(T), ctypes.c_uint64(seed),
                           ctypes.c_int32(t0), _p(self.pos), _p(self.goal), _p(self.done),

@@ -73,7 +73,7 @@ static int in_bounds(const orc_cfg* c, int r, int col) {
  * (the reference asserts before touching state, :91-92). */
 static int step_env(const orc_cfg* c, int64_t e, int32_t* pos, const int32_t* goal, uint8_t* done,
                     int32_t* t, int32_t* steps, const uint8_t* bits, const int32_t* act,
-                    double* reward, uint8_t* node_out, uint8_t* edge_out, int32_t* occ,
+                    double* reward, uint8_t* node_out, uint16_t* edge_out, int32_t* occ,
                     int32_t* newp, double* rew, int32_t* cnt) {
   const int N = c->N, H = c->H, W = c->W;
   for (int i = 0; i < N; ++i)
@@ -123,7 +123,7 @@ static int step_env(const orc_cfg* c, int64_t e, int32_t* pos, const int32_t* go
     rew[i] = rew[i] + c->collide_rew * (double)node; /* :127-130 */
     rew[i] = rew[i] + c->collide_rew * (double)edge;
     if (node_out) node_out[i] = (uint8_t)node;
-    if (edge_out) edge_out[i] = (uint8_t)(edge > 255 ? 255 : edge);
+    if (edge_out) edge_out[i] = (uint16_t)edge; /* <= N - 1 < 2^16: exact */
   }
   double R = 0.0; /* sum(rewards): naive left fold (:141, CPython <= 3.11) */
   for (int i = 0; i < N; ++i) R = R + rew[i];
@@ -239,7 +239,7 @@ static void observe_env(const orc_cfg* c, const int32_t* pos, const int32_t* goa
  * rejected for an out-of-range action (left unchanged). */
 int orc_step(const orc_cfg* c, int32_t* pos, const int32_t* goal, uint8_t* done, int32_t* t,
              int32_t* steps, const uint8_t* bits, const int32_t* actions, double* reward,
-             uint8_t* node, uint8_t* edge, int nthreads) {
+             uint8_t* node, uint16_t* edge, int nthreads) {
   const int N = c->N;
   int bad = 0;
 #pragma omp parallel num_threads(nthreads) reduction(+ : bad)
@@ -302,7 +302,7 @@ int orc_observe(const orc_cfg* c, const int32_t* pos, const int32_t* goal, const
  * step's values. */
 int orc_rollout(const orc_cfg* c, int32_t T, uint64_t seed, int32_t t0, int32_t* pos,
                 const int32_t* goal, uint8_t* done, int32_t* t, int32_t* steps,
-                const uint8_t* bits, double* reward, uint8_t* node, uint8_t* edge,
+                const uint8_t* bits, double* reward, uint8_t* node, uint16_t* edge,
                 uint8_t* avail, void* obs_window, int window, int nthreads) {
   const int N = c->N;
   const int es = N > 127 ? 2 : 1;

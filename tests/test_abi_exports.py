@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     exported = set(re.findall(r"\bT (mapfx_\w+)", nm))
     missing = set(declared) - exported
     assert not missing, missing
-    assert mapfx.lib.mapfx_abi_version() == 2
+    assert mapfx.lib.mapfx_abi_version() == 3
 
 
 def test_host_helpers():
@@ -39,6 +39,9 @@ def test_host_helpers():
     assert lib.mapfx_obs_elem_size(16) == 1
     assert lib.mapfx_obs_elem_size(127) == 1
     assert lib.mapfx_obs_elem_size(128) == 2
+    # an edge count is at most N - 1: exact in u8 up to N = 256, u16 above
+    assert lib.mapfx_edge_elem_size(256) == 1
+    assert lib.mapfx_edge_elem_size(257) == 2
 
 
 def test_action_generator_host_vs_numpy():

@@ -713,3 +713,63 @@ def test_wave_partial_lane_groups(mapfx_mod, N):
             assert np.array_equal(_np(got["avail"]), ref["avail"]), (N, t)
             assert np.array_equal(_np(got["obs_window"]), ref["obs_window"]), (N, t)
         assert np.array_equal(_np(b.pos), ob.pos), (N, t)
+
+
+@pytest.mark.parametrize("N", [256, 300])
+def test_stacked_swap_edge_count_exact(mapfx_mod, N):
+    """__count_edge_collision (:364-383) counts every stacked agent that swaps
+    back: N - 1 agents stacked on one cell move right while the agent on the
+    right moves left, so that agent's edge count is N - 1 (255 at N = 256, the
+    u8 limit; 299 at N = 300, where `edge` is u16, mapfx_edge_elem_size)."""
+    from oracle import corc
+    from mapfx.maps import pack_bits
+    E, S = 3, 20
+    init = np.zeros((E, N, 2), np.int32)
+    init[:, :, :] = (5, 5)
+    init[:, N - 1] = (5, 6)
+    goals = np.zeros((E, N, 2), np.int32)
+    goals[:, :, :] = (15, 15)
+    bits = pack_bits(np.zeros((1, S, S), np.int8))
+    b = mapfx_mod.MapfGridBatch(init, goals, bits=bits, hw=(S, S), obs=("window",), window=5)
+    ob = corc.OracleBatch(bits, init, goals, S, S)
+    b.reset()
+    a = np.full((E, N), 3, np.int8)
+    a[:, N - 1] = 2
+    a[1, :] = 4                                  # env 1 stays: no collisions
+    out = b.step(torch.from_numpy(a).cuda())
+    ref = ob.step(a.astype(np.int32))
+    edge = _np(out["edge"]).astype(np.int64)
+    assert edge[0, N - 1] == N - 1 and (edge[0, :N - 1] == 1).all()
+    assert (edge[1] == 0).all()
+    assert np.array_equal(edge, ref["edge"].astype(np.int64))
+    assert np.array_equal(_u64(_np(out["reward"])), _u64(ref["reward"]))
+    assert out["edge"].dtype == (torch.uint8 if N <= 256 else torch.int16)
+    # the fused rollout (same kernel body, trajectory slots) agrees
+    b2 = mapfx_mod.MapfGridBatch(init, goals, bits=bits, hw=(S, S), obs=("window",), window=5)
+    b2.reset()
+    traj = b2.rollout(1, actions=torch.from_numpy(a[None]).cuda())
+    assert np.array_equal(_np(traj["edge"][0]).astype(np.int64), edge)
+
+
+def test_rollout_does_not_pin_trajectories(mapfx_mod):
+    """rollout() without a caller buffer allocates a fresh trajectory per
+    call; the batch must not keep those alive (device memory stays flat)."""
+    from mapfx.maps import synthetic_instances
+    inst = synthetic_instances(256, 16, 16, 8, p_obstacle=0.1, seed=2)
+    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(16, 16),
+                                obs=("window",), window=5)
+    b.reset()
+    for _ in range(3):
+        b.rollout(8, seed=1)
+    torch.cuda.synchronize()
+    m0 = torch.cuda.memory_allocated()
+    for _ in range(80):
+        b.rollout(8, seed=1)
+    torch.cuda.synchronize()
+    assert torch.cuda.memory_allocated() == m0
+    # a caller-owned buffer is still reused through the struct cache
+    traj = b._alloc_out(8)
+    b.rollout(8, seed=1, traj=traj)
+    n = len(b._traj_cache)
+    b.rollout(8, seed=1, traj=traj)
+    assert len(b._traj_cache) == n

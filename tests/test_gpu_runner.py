@@ -53,17 +53,14 @@ class Logger:
         self.stats.append((k, float(v), int(t)))
 
 
-@pytest.mark.parametrize("name", CASES)
-def test_runner_matches_reference_parallel_runner(tmp_path, name):
-    from conftest import load_fixture
+def _make_runner(tmp_path, fx, B, mac, **extra):
     from mapfx.episode import DeviceEpisodeBatch, OneHot
     from mapfx.runners import ParallelRunner
-    fx = load_fixture(name)
     rows = [str(r) for r in fx["map"]]
     s = len(rows)
     mp = tmp_path / "m.map"
     mp.write_text("type octile\nheight %d\nwidth %d\nmap\n%s\n" % (s, s, "\n".join(rows)))
-    B, N, limit = int(fx["B"]), int(fx["n_agents"]), int(fx["limit"])
+    N, limit = int(fx["n_agents"]), int(fx["limit"])
     starts, goals = fx["inst_starts"], fx["inst_goals"]   # [episodes, N, 2], one per run
 
     def instance_fn(ep):
@@ -75,7 +72,7 @@ def test_runner_matches_reference_parallel_runner(tmp_path, name):
         env_args=dict(REWARDS, grid_file_path=str(mp), agents_path=str(tmp_path / "x-"),
                       n_agents=N, obs_window=int(fx["obs_window"]),
                       obs_knn_agents=int(fx["obs_knn_agents"]), episode_limit=limit),
-        episode_batch_cls=DeviceEpisodeBatch, test_nepisode=B, runner_log_interval=1)
+        episode_batch_cls=DeviceEpisodeBatch, test_nepisode=B, runner_log_interval=1, **extra)
     logger = Logger()
     runner = ParallelRunner(args, logger, instance_fn=instance_fn)
     info = runner.get_env_info()
@@ -84,8 +81,15 @@ def test_runner_matches_reference_parallel_runner(tmp_path, name):
               "actions": {"vshape": (1,), "group": "agents", "dtype": torch.long},
               "avail_actions": {"vshape": (info["n_actions"],), "group": "agents", "dtype": torch.int},
               "reward": {"vshape": (1,)}, "terminated": {"vshape": (1,), "dtype": torch.uint8}}
-    runner.setup(scheme, {"agents": N}, {"actions": ("actions_onehot", [OneHot(out_dim=5)])},
-                 ScriptedMAC())
+    runner.setup(scheme, {"agents": N}, {"actions": ("actions_onehot", [OneHot(out_dim=5)])}, mac)
+    return runner, logger
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_runner_matches_reference_parallel_runner(tmp_path, name):
+    from conftest import load_fixture
+    fx = load_fixture(name)
+    runner, logger = _make_runner(tmp_path, fx, int(fx["B"]), ScriptedMAC())
     for r in range(int(fx["runs"])):
         batch = runner.run(test_mode=False)
         for k, v in batch.data.transition_data.items():
@@ -97,6 +101,93 @@ def test_runner_matches_reference_parallel_runner(tmp_path, name):
     assert [k for k, _, _ in logger.stats] == fx["log_stats"].tolist()
     assert [v for _, v, _ in logger.stats] == fx["log_values"].tolist()
     assert [t for _, _, t in logger.stats] == fx["log_t"].tolist()
+
+
+class TiledMAC:
+    """ScriptedMAC for a batch that tiles a fixture's B_fx envs: env b acts as
+    fixture env b % B_fx (the same scripted_action), vectorised on the device so
+    the runner loop stays free of host reads.  Accepts a padded or exact `bs`."""
+
+    action_selector = types.SimpleNamespace()
+
+    def __init__(self, bfx):
+        self.bfx = bfx
+
+    def init_hidden(self, batch_size):
+        pass
+
+    def select_actions(self, batch, t_ep, t_env, bs, test_mode=False):
+        avail = batch["avail_actions"][:, t_ep]                 # [B, N, 5] int32
+        bb = bs % self.bfx
+        n = torch.arange(avail.shape[1], device=avail.device)
+        a = (3 * bb[:, None] + 7 * t_ep + 5 * n[None, :] + ((bb * t_ep) % 3)[:, None]) % 5
+        ok = torch.gather(avail[bs], 2, a[..., None]).squeeze(-1) != 0
+        return torch.where(ok, a, torch.full_like(a, 4))
+
+
+@pytest.mark.parametrize("B", [4096, 1100])
+@pytest.mark.parametrize("name", CASES)
+def test_runner_tiled_matches_reference_at_bench_shape(tmp_path, name, B):
+    """the runner's multi-wave `bs` compaction (runner.hip, per-thread
+    chunks + wave scans, reached only at large B) pinned at the bench's B = 4096 and
+    at a ragged B = 1100.  Every env of the batch is the fixture instance and acts
+    as fixture env b % B_fx, so env b's rows must equal the REFERENCE runner's rows
+    of env b % B_fx byte for byte (envs never interact), every run.  Per-env returns
+    and lengths must equal those of the B_fx-env run (itself pinned to the fixture's
+    t_env and logged stats), so t_env and the logged stats follow exactly."""
+    from conftest import load_fixture
+    fx = load_fixture(name)
+    bfx = int(fx["B"])
+    (tmp_path / "base").mkdir()
+    base, _ = _make_runner(tmp_path / "base", fx, bfx, TiledMAC(bfx))
+    tiled, logger = _make_runner(tmp_path, fx, B, TiledMAC(bfx))
+    src = np.arange(B) % bfx
+    t_env = 0
+    exp_log = []
+    for r in range(int(fx["runs"])):
+        base.run(test_mode=False)
+        assert base.t_env == int(fx["run%d_t_env" % r])
+        blen = base._ep_length.cpu().numpy()
+        bret = base._ep_return.cpu().numpy()
+        batch = tiled.run(test_mode=False)
+        for k, v in batch.data.transition_data.items():
+            ref = fx["run%d_%s" % (r, k)][src]
+            got = v.cpu().numpy()
+            assert got.shape == ref.shape and got.dtype == ref.dtype, (r, k)
+            assert np.array_equal(got.view(np.uint8), ref.view(np.uint8)), (r, k, B)
+        assert np.array_equal(tiled._ep_length.cpu().numpy(), blen[src]), r
+        assert np.array_equal(tiled._ep_return.cpu().numpy().view(np.uint64),
+                              bret[src].view(np.uint64)), r
+        t_env += int(blen[src].sum())
+        assert tiled.t_env == t_env
+        rets = bret[src].tolist()
+        total_len = int(blen[src].sum())
+        exp_log += [("return_mean", float(np.mean(rets)), t_env),
+                    ("return_std", float(np.std(rets)), t_env),
+                    ("_step_count_mean", total_len / B, t_env),
+                    ("ep_length_mean", total_len / B, t_env)]
+    assert logger.stats == exp_log
+
+
+def test_runner_exact_bs_mode(tmp_path):
+    """args.runner_exact_bs: the MAC gets bs[:len(bs)], rows unchanged."""
+    from conftest import load_fixture
+    fx = load_fixture("runner_open5_n2")
+    bfx, B = int(fx["B"]), 1100
+    seen = []
+
+    class Recording(TiledMAC):
+        def select_actions(self, batch, t_ep, t_env, bs, test_mode=False):
+            seen.append(int(bs.shape[0]))
+            return super().select_actions(batch, t_ep, t_env, bs, test_mode)
+
+    runner, _ = _make_runner(tmp_path, fx, B, Recording(bfx), runner_exact_bs=True)
+    batch = runner.run(test_mode=False)
+    src = np.arange(B) % bfx
+    for k, v in batch.data.transition_data.items():
+        assert np.array_equal(v.cpu().numpy().view(np.uint8),
+                              fx["run0_%s" % k][src].view(np.uint8)), k
+    assert seen[0] == B and min(seen) < B      # shrinks once envs terminate
 
 
 def test_runner_step_needs_no_host_sync(tmp_path, monkeypatch):

@@ -64,6 +64,11 @@ def parse():
                     help="target CPU work of the cpu_baseline sample (0 disables)")
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: skip the RCCL gather leg (reported beside the compute-only value)")
+    ap.add_argument("--gather-payload", default="occ", choices=("occ", "planes", "reward_done"),
+                    help="what each chunk gathers to rank 0: occ = obs_window_occ (the window as "
+                         "one occupancy plane, half the bytes of the two planes) + reward + done; "
+                         "planes = obs_window + reward + done; reward_done = reward + done only "
+                         "(observations consumed on-rank)")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank launch + shard + packed gather")
     ap.add_argument("--selftest-envs", type=int, default=6)
@@ -370,7 +375,18 @@ def main():
     # ---- RCCL gather of (obs, reward, done) to rank 0 (N > 1: on by default) ----
     gather = None
     if dist and not args.no_gather:
-        gather = time_gather(dist, b, acts, outs, T, n_wu * T, K, world, E, N, wkey)
+        gb, gouts, gkeys = b, outs, (wkey, "reward", "traj_done")
+        if args.gather_payload == "reward_done":
+            gkeys = ("reward", "traj_done")
+        elif args.gather_payload == "occ" and wkind != "window_occ":
+            gb = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                                     episode_limit=limit, obs=("window_occ",), window=W,
+                                     device="cuda:%d" % local, env_offset=offset, track_steps=False)
+            gb.reset()
+            gouts = tuple("obs_window_occ" if k == wkey else k for k in outs)
+            gkeys = ("obs_window_occ", "reward", "traj_done")
+        gather = time_gather(dist, gb, acts, gouts, T, n_wu * T, K, world, E, N, gkeys,
+                             args.gather_payload)
 
     # ---- CPU baseline: the oracle's C restatement on this host (rank 0, N=1) ----
     cpu = None
@@ -444,13 +460,19 @@ def main():
         dist.destroy_process_group()
 
 
-def time_gather(dist, b, acts, outs, T, k0, K, world, E, N, wkey="obs_window"):
-    """The same K env steps as rollout chunks of T, each chunk's (window obs,
-    reward, done) packed in one buffer and gathered to rank 0 with ONE RCCL gather
-    on a side stream, overlapped with the next chunk (mapfx.dist.OverlappedGather).
-    Rank 0 orders a read of every chunk after its gather (stream wait, no sync)."""
+# rank 0's xGMI ingress: 7 peers x one ~153 GB/s link each
+XGMI_LINK_GBS = 153.0
+
+
+def time_gather(dist, b, acts, outs, T, k0, K, world, E, N, keys, payload):
+    """The same K env steps as rollout chunks of T, each chunk's gathered outputs
+    (`keys`: window obs, reward, done) packed in one buffer and gathered to rank 0 with
+    ONE RCCL gather on a side stream, overlapped with the next chunk
+    (mapfx.dist.OverlappedGather).  Rank 0 orders a read of every chunk after its
+    gather (stream wait, no sync).  The ingress bound: rank 0 receives (world - 1)
+    chunks per chunk time over at most (world - 1) links."""
     from mapfx.dist import OverlappedGather
-    og = OverlappedGather(b, T, keys=(wkey, "reward", "traj_done"), outputs=outs)
+    og = OverlappedGather(b, T, keys=keys, outputs=outs)
     og.step_chunk(actions=acts[:T])                  # warm the communicator
     og.result(0)
     torch.cuda.synchronize()
@@ -467,12 +489,17 @@ def time_gather(dist, b, acts, outs, T, k0, K, world, E, N, wkey="obs_window"):
     t = torch.tensor([el], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
+    per_chunk = int(og.bytes_per_chunk())
+    ingress = (world - 1) * per_chunk
     return {"value": round(world * E * N * nch * T / el, 1),
             "ms_per_step": round(el / (nch * T) * 1e3, 5),
-            "steps": nch * T, "chunk_steps": T,
-            "bytes_per_rank_per_chunk": int(og.bytes_per_chunk()),
+            "steps": nch * T, "chunk_steps": T, "payload": payload, "keys": list(keys),
+            "bytes_per_rank_per_chunk": per_chunk,
+            "rank0_ingress_bytes_per_chunk": ingress,
+            "ingress_bound_ms_per_chunk": round(ingress / (max(1, world - 1) * XGMI_LINK_GBS * 1e9)
+                                                * 1e3, 5),
             "collective": "one torch.distributed.gather (RCCL) per chunk to rank 0 on a side "
-                          "stream, packed (obs_window, reward, done) buffer"}
+                          "stream, packed %s buffer" % "+".join(keys)}
 
 
 PARTIAL_YAML = dict(  # MARL-curve-main/src/config/envs/marl_partial.yaml:3-23

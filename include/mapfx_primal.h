@@ -11,8 +11,14 @@
  *     State.moveAgent :103-135, reward table :579-596, _observe :343-386,
  *     State.done :159-166, _listNextValidActions :639-667
  *
- * Actions: 0 stay, 1 (0,+1), 2 (+1,0), 3 (0,-1), 4 (-1,0) (dirDict, :28).
- * JOINT = False and DIAGONAL_MOVEMENT = False (the reference defaults, :27, :175).
+ * Actions: 0 stay, 1 (0,+1), 2 (+1,0), 3 (0,-1), 4 (-1,0) (dirDict, :28); with
+ * cfg.diagonal (DIAGONAL_MOVEMENT, :175) also 5 (1,1), 6 (1,-1), 7 (-1,-1), 8 (-1,1):
+ * then every move is also refused (-3) when it crosses another agent's last move
+ * (State.diagonalCollision :77-99: equal midpoints of (past, present) and (old, new);
+ * with integer coordinates np.isclose of the halves is exact equality of the sums),
+ * each agent's past position (agents_past) is part of the state, updated by a stay
+ * and by a successful move (:110-112, :129-131), and next_mask has 9 bits (u16).
+ * JOINT = False (the reference default, :27).
  * The stay-on-goal blocking term (:583, get_blocking_reward) needs the
  * un-vendored od_mstar3 planner and is defined as 0 (parity unpinned); the
  * `blocking` output of _step is therefore always False and not produced.
@@ -39,19 +45,23 @@ typedef struct mapfx_primal_cfg {
   int32_t n_envs;        /* E worlds                                             */
   int32_t obs_size;      /* observation_size s (:175)                            */
   int32_t map_shared;    /* 1: one obstacle map for all worlds                   */
+  int32_t diagonal;      /* DIAGONAL_MOVEMENT (:175): 9 actions, agents_past     */
 } mapfx_primal_cfg;
 
 typedef struct mapfx_primal_state {
   int32_t* pos;             /* [E][N][2] (row, col), updated in place             */
   const int32_t* goal;      /* [E][N][2]                                          */
   const uint8_t* map_bits;  /* [E or 1][mapfx_map_stride(H, W)] obstacle bitmaps  */
+  int32_t* past;            /* [E][N][2] agents_past (cfg.diagonal only; updated in
+                               place; set it equal to pos for a fresh world, :55-66) */
 } mapfx_primal_state;
 
 /* Outputs of the k-th call of world e at index [e][k] (NULL = not produced). */
 typedef struct mapfx_primal_out {
   double* reward;        /* [E][K]                                               */
   uint8_t* done;         /* [E][K] world.done() after the call                   */
-  uint8_t* next_mask;    /* [E][K] bit a = action a in _listNextValidActions     */
+  uint8_t* next_mask;    /* [E][K] bit a = action a in _listNextValidActions; u8,
+                            or u16 ([E][K] uint16_t) with cfg.diagonal (9 bits)   */
   uint8_t* on_goal;      /* [E][K]                                               */
   uint8_t* valid;        /* [E][K] action_status >= 0                            */
   uint8_t* obs;          /* [E][K][4][s][s] _observe maps (poss, goal, goals, obs) */

@@ -1153,6 +1153,60 @@ __device__ __forceinline__ void window_regs(const uint32_t* qx, int o, uint32_t 
   }
 }
 
+// ---- occupancy window records (obs_window_occ, ABI 2) ------------------------
+// The record of one agent is WIN*WIN bytes, one per window cell: occ = c - 1 (the
+// reference's map value: -1 for an obstacle nobody stands on or a cell out of
+// bounds, else the agent count), marl_partial.py:323-342 as one plane.
+__device__ __forceinline__ uint32_t swar_occ(uint32_t v) {  // 4 cells -> 4 occ bytes (c - 1)
+  return (((v & 0x7F7F7F7Fu) | 0x80808080u) - 0x01010101u) ^ 0x80808080u;
+}
+// Record bytes as u32 words from the raw rows (qx as for window_regs).
+template <int WIN>
+__device__ __forceinline__ void occ_words(const uint32_t* qx, int o, uint32_t (&R)[(WIN * WIN + 3) / 4 + 1]) {
+  constexpr int NW64 = (WIN * WIN + 7) / 8;
+  uint64_t w[NW64];
+#pragma unroll
+  for (int i = 0; i < NW64; ++i) w[i] = 0;
+#pragma unroll
+  for (int y = 0; y < WIN; ++y) {
+    const uint32_t lo = swar_occ(__builtin_amdgcn_alignbyte(qx[WIN + y], qx[y], o));  // cells 0-3
+    if constexpr (WIN == 3) {
+      put_bits<NW64>(w, 24 * y, 24, lo & 0xFFFFFFu);
+    } else {
+      const uint32_t hi = WIN == 5 ? swar_occ(__builtin_amdgcn_alignbyte(0u, qx[WIN + y], o))
+                                   : swar_occ(__builtin_amdgcn_alignbyte(qx[2 * WIN + y], qx[WIN + y], o));
+      put_bits<NW64>(w, 8 * WIN * y, 32, lo);
+      put_bits<NW64>(w, 8 * WIN * y + 32, 8 * (WIN - 4), hi & ((1u << (8 * (WIN - 4))) - 1u));
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < (WIN * WIN + 3) / 4 + 1; ++k)
+    R[k] = k / 2 < NW64 ? (uint32_t)(w[k / 2] >> (32 * (k & 1))) : 0u;
+}
+// Stage one WIN*WIN-byte record at byte `ra` of LDS (odd length, any alignment):
+// h = head bytes up to the next dword boundary (0..3), then ND aligned dwords, then
+// the tail; with REC = 1 mod 8 the head and tail together are always 5 bytes, so
+// every lane issues ND ds_write_b32 + 5 ds_write_b8 (no divergence).
+template <int WIN>
+__device__ __forceinline__ void stage_occ_record(const uint32_t (&R)[(WIN * WIN + 3) / 4 + 1], uint32_t ra) {
+  typedef __attribute__((address_space(3))) uint32_t lds_u32;
+  typedef __attribute__((address_space(3))) uint8_t lds_u8;
+  constexpr int REC = WIN * WIN;
+  constexpr int ND = (REC - 3) / 4;
+  static_assert(REC - 4 * ND == 5, "odd window: head + tail = 5 bytes");
+  const uint32_t h = (4u - (ra & 3u)) & 3u;
+  lds_u32* d = (lds_u32*)(uintptr_t)(ra + h);
+#pragma unroll
+  for (int j = 0; j < ND; ++j) d[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], h);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const bool head = (uint32_t)i < h;
+    const uint32_t hv = R[0] >> (8 * (i & 3));                                   // byte i
+    const uint32_t tv = R[(4 * ND + i) >> 2] >> (8 * ((4 * ND + i) & 3));      // byte 4 ND + i
+    *(lds_u8*)(uintptr_t)(ra + (head ? (uint32_t)i : (uint32_t)(4 * ND + i))) = (uint8_t)(head ? hv : tv);
+  }
+}
+
 // ---- store-wave split (runner rollout, N = 16) --------------------------------
 // The wave that steps the envs (the "step wave") keeps only the dependency chain
 // of a step: moves, LDS count atomics, edge collisions (a cross-lane scan) and
@@ -1246,7 +1300,7 @@ __device__ __forceinline__ int2 padded_cell_rc(const Geo& g, int cell) {
 //     fold is an in-row DPP scan (row_fold16), lane LL-1 of each env stores it.
 constexpr int ROLE_ALL = 0, ROLE_REC = 1, ROLE_SMALL = 2;
 
-template <int WIN, int LL, int ROLE>
+template <int WIN, int LL, int ROLE, bool OCC = false>
 __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, unsigned char* sp,
                                                  unsigned char* own, int env0, int lane) {
   typedef __attribute__((address_space(1))) unsigned char gbyte;  // global_store, not flat_
@@ -1254,7 +1308,8 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
   typedef int i32x2 __attribute__((ext_vector_type(2)));
   using SL = SplitLayout<WIN, LL>;
   constexpr bool RECS = ROLE != ROLE_SMALL, SMALL = ROLE != ROLE_REC;
-  constexpr int H2 = WIN / 2, REC = SL::REC, NQ = SL::SLOT / 16;
+  // OCC: obs_window_occ records (WIN*WIN bytes, one occupancy plane), else obs_window
+  constexpr int H2 = WIN / 2, REC = OCC ? WIN * WIN : SL::REC, NQ = SL::SLOT / 16;
   constexpr int RCH = 4 * REC;                  // 16-byte chunks of the wave's 64 records
   constexpr int NRC = (RCH + 63) / 64;          // chunk rounds per lane
   constexpr int IMG = 64 * REC;                 // one staged-record image
@@ -1271,7 +1326,7 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
       rv[k] = ost[(p & 1) * (IMG / 16) + ((k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0)];
   };
   auto store_recs = [&](uint32_t p, const u32x4 (&rv)[NRC], bool ok) {
-    gbyte* rec = (gbyte*)a.obs_window + (p * EN + ag0) * (uint32_t)REC;
+    gbyte* rec = (gbyte*)(OCC ? a.obs_window_occ : a.obs_window) + (p * EN + ag0) * (uint32_t)REC;
 #pragma unroll
     for (int k = 0; k < NRC; ++k)
       if (ok && (k < NRC - 1 || lane + 64 * k < RCH))
@@ -1300,7 +1355,12 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
     const uint32_t nb = w[1], fl = w[2];
     const uint32_t* qx = w + 4;
     const int o = (nc - H2) & 3;
-    if constexpr (RECS) {
+    if constexpr (RECS && OCC) {
+      uint32_t R[(WIN * WIN + 3) / 4 + 1];
+      occ_words<WIN>(qx, o, R);
+      store_recs(q - 1, rv, q > 0);
+      stage_occ_record<WIN>(R, lds_addr(own + (q & 1) * IMG + lane * REC));
+    } else if constexpr (RECS) {
       uint32_t R[4 * WIN];
       window_regs<WIN>(qx, o, R);
       store_recs(q - 1, rv, q > 0);
@@ -1380,20 +1440,21 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
 #ifndef MAPFX_PRIO_STORE
 #define MAPFX_PRIO_STORE 3
 #endif
-template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false>
+template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false, bool OCC = false>
 __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g0) {
   Args a = a0;
   Geo g = g0;
   MAPFX_HOT_APPLY(a, g);
   extern __shared__ __align__(16) unsigned char lds[];
   static_assert(!SPLIT || (ROLL && FULLW && RUNNER && LL == 16 && WIN > 0), "split: runner rollout, N = 16");
+  static_assert(!OCC || (SPLIT && MAPFX_SPLIT_WAVES == 2), "occupancy records: two-wave split only");
   if constexpr (SPLIT) {
     if (threadIdx.x >= 64) {  // the output side of the split
       if (MAPFX_PRIO_STORE) __builtin_amdgcn_s_setprio(MAPFX_PRIO_STORE);
       const int e0 = xcd_block(blockIdx.x, g.nblk) * (64 / LL);
       unsigned char* sp = lds + g.wv_off_split;
       unsigned char* own = sp + 2 * g.wv_split_buf;
-      if (MAPFX_SPLIT_WAVES == 2) split_store_wave<WIN, LL, ROLE_ALL>(g, a, sp, own, e0, threadIdx.x & 63);
+      if (MAPFX_SPLIT_WAVES == 2) split_store_wave<WIN, LL, ROLE_ALL, OCC>(g, a, sp, own, e0, threadIdx.x & 63);
       else if (threadIdx.x < 128) split_store_wave<WIN, LL, ROLE_REC>(g, a, sp, own, e0, threadIdx.x & 63);
       else split_store_wave<WIN, LL, ROLE_SMALL>(g, a, sp, own, e0, threadIdx.x & 63);
       return;
@@ -2018,7 +2079,13 @@ int check_hip(hipError_t e, const char* what) {
 
 
 template <int WIN>
-KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split) {
+KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split, bool occ) {
+  if (occ) {  // obs_window_occ: only the store-wave split writes it on the wave path
+    if constexpr (WIN > 0 && MAPFX_SPLIT_WAVES == 2) {
+      if (roll && runner && split && fullw && L == 16) return mapf_wave_kernel<WIN, true, true, true, 16, true, true>;
+    }
+    return nullptr;
+  }
   if (roll) {
     if (runner) {
       if constexpr (WIN > 0) {
@@ -2035,12 +2102,12 @@ KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split) {
   return fullw ? mapf_wave_kernel<WIN, false, true, false, 0> : mapf_wave_kernel<WIN, false, false, false, 0>;
 }
 
-KernelFn pick_wave_kernel(int win, bool roll, bool fullw, bool runner, int L, bool split) {
+KernelFn pick_wave_kernel(int win, bool roll, bool fullw, bool runner, int L, bool split, bool occ) {
   switch (win) {
-    case 0: return pick_wave_win<0>(roll, fullw, runner, L, split);
-    case 3: return pick_wave_win<3>(roll, fullw, runner, L, split);
-    case 5: return pick_wave_win<5>(roll, fullw, runner, L, split);
-    case 7: return pick_wave_win<7>(roll, fullw, runner, L, split);
+    case 0: return pick_wave_win<0>(roll, fullw, runner, L, split, occ);
+    case 3: return pick_wave_win<3>(roll, fullw, runner, L, split, occ);
+    case 5: return pick_wave_win<5>(roll, fullw, runner, L, split, occ);
+    case 7: return pick_wave_win<7>(roll, fullw, runner, L, split, occ);
   }
   return nullptr;
 }
@@ -2053,17 +2120,19 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
   const long long slot_elems = (long long)(roll ? a.T : 1) * g.E * g.N;
   const bool fits32 = slot_elems * std::max(8, 2 * g.window * g.window) < (1ll << 31) &&
                       (long long)(roll ? a.T : 1) * g.E * g.H * g.W < (1ll << 31);
-  if (g.wave_ok && fits32 && !a.obs_primal && !a.primal_vec && !a.obs_window_occ) {
+  if (g.wave_ok && fits32 && !a.obs_primal && !a.primal_vec && !(a.obs_window && a.obs_window_occ)) {
     const bool fullw = g.N == g.L && g.E % g.EPW == 0;
+    const bool occ = a.obs_window_occ != nullptr;
     const bool runner = roll && a.reward && a.term && a.node && a.edge && a.avail &&
-                        a.traj_pos && a.traj_done && a.traj_t && a.obs_window && !a.obs_full;
-    const uintptr_t al16 = (uintptr_t)a.obs_window | (uintptr_t)a.traj_pos | (uintptr_t)a.node |
-                           (uintptr_t)a.edge | (uintptr_t)a.avail | (uintptr_t)a.traj_done |
-                           (uintptr_t)a.reward | (uintptr_t)a.traj_t;
-    const int split_lds = g.wv_lds + 2 * g.wv_split_buf + 2 * 64 * g.wlen;  // + staged-record images
+                        a.traj_pos && a.traj_done && a.traj_t && (a.obs_window || occ) && !a.obs_full;
+    const uintptr_t al16 = (uintptr_t)a.obs_window | (uintptr_t)a.obs_window_occ | (uintptr_t)a.traj_pos |
+                           (uintptr_t)a.node | (uintptr_t)a.edge | (uintptr_t)a.avail |
+                           (uintptr_t)a.traj_done | (uintptr_t)a.reward | (uintptr_t)a.traj_t;
+    // + staged-record images of the store wave (2 x 64 records)
+    const int split_lds = g.wv_lds + 2 * g.wv_split_buf + 2 * 64 * (occ ? g.wlen / 2 : g.wlen);
     const bool split = MAPFX_SPLIT && runner && fullw && g.L == 16 && g.wv_split_buf > 0 &&
                        split_lds <= 64 * 1024 && (al16 & 15) == 0;
-    KernelFn fn = pick_wave_kernel(a.obs_window ? g.window : 0, roll, fullw, runner, g.L, split);
+    KernelFn fn = pick_wave_kernel((a.obs_window || occ) ? g.window : 0, roll, fullw, runner, g.L, split, occ);
     if (fn) {
       const int blocks = (g.E + g.EPW - 1) / g.EPW;
       const dim3 bt(split ? 64 * MAPFX_SPLIT_WAVES : 64);

@@ -9,12 +9,19 @@
 // later call sees the moves of the earlier ones.
 //
 // One lane group of 16, 32 or 64 lanes per world, 64 / lw worlds per wave.  The
-// world lives in LDS as an occupant map (0 empty, id + 1) and an obstacle bitmap;
-// for each call the group's first lane resolves the move (the only sequential
-// part) and the group builds that agent's 4 x s x s observation (one cell per
-// lane), the visible agents' clamped goals (one agent per lane) and the done
-// ballot.  The goal-vector magnitude comes from a host
-// libm pow LUT, as the reference computes `(dx**2 + dy**2) ** .5` (quirk 8).
+// world lives in LDS as a PADDED byte map (bit 0 agent, bit 1 wall or outside the
+// grid: PRIMAL's state array, :38-45, with the out-of-bounds test of :356-359 as a
+// border of walls) and the agents' (position, goal) records; each lane also holds
+// its own agents (and, for DIAGONAL_MOVEMENT, their past positions) in registers.
+// Per call every lane of the world resolves State.moveAgent itself from broadcast
+// LDS reads (no status hand-off), then produces 4 bytes of each observation plane
+// with SWAR on one realigned map dword (s even: a plane row of s cells is s / 4
+// dwords, so lane m writes cells 4m .. 4m + 3 of each plane with ONE dword store),
+// stamps the visible agents' clamped goals into a per-world window image, and the
+// world's scalar outputs (reward, done, next-action mask, on_goal, valid, goal
+// vector) are staged in LDS and leave once per 64-call block as coalesced runs.
+// The goal-vector magnitude comes from a host libm pow LUT, as the reference
+// computes `(dx**2 + dy**2) ** .5` (quirk 8).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -39,12 +46,17 @@ struct QGeo {
   long long map_stride;
   int hw, bits_words, lut_n;
   int lw, lw_shift, wreg;  // lanes per world (16 / 32 / 64), log2, LDS bytes per world
+  int P, PW, rows;         // padded byte map: rows x PW, interior at (P, P); P >= max(1, s / 2)
+  int off_bm, off_goals, off_ag, off_pair, off_pend, off_rst, off_fst;  // regions of a world
+  int diag, nact, apl;     // DIAGONAL_MOVEMENT, actions (5 / 9), agents per lane
+  uint64_t m_s, m_ss;      // fastdiv magics (odd s path)
 };
 
 struct QArgs {
   int32_t* pos;
   const int32_t* goal;
   const uint8_t* bits;
+  int32_t* past;
   const int32_t* ids;
   const int32_t* acts;
   int K;
@@ -65,60 +77,117 @@ __device__ inline void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ inline int dir_r(int a) { return a == 2 ? 1 : (a == 4 ? -1 : 0); }  // dirDict :28
-__device__ inline int dir_c(int a) { return a == 1 ? 1 : (a == 3 ? -1 : 0); }
+// dirDict (:28) as 2-bit fields of (d + 1), action a at bits 2a:
+// a:      0  1  2  3  4  5  6  7  8
+// row+1:  1  1  2  1  0  2  2  0  0      col+1:  1  2  1  0  1  2  0  0  2
+constexpr uint32_t DR1 = 1u | 1u << 2 | 2u << 4 | 1u << 6 | 0u << 8 | 2u << 10 | 2u << 12 | 0u << 14 | 0u << 16;
+constexpr uint32_t DC1 = 1u | 2u << 2 | 1u << 4 | 0u << 6 | 1u << 8 | 2u << 10 | 0u << 12 | 0u << 14 | 2u << 16;
+__device__ inline int dir_r(int a) { return (int)((DR1 >> (2 * a)) & 3u) - 1; }
+__device__ inline int dir_c(int a) { return (int)((DC1 >> (2 * a)) & 3u) - 1; }
+// opposite_actions (:26): 1<->3, 2<->4, 5<->7, 6<->8; 0 has none
+__device__ inline int opposite(int a) { return a == 0 ? -1 : (a <= 4 ? ((a + 1) & 3) + 1 : ((a - 3) & 3) + 5); }
+// the action whose direction is (dr, dc), |dr|, |dc| <= 1 (index (dr + 1) * 3 + dc + 1), 0 for (0, 0)
+constexpr uint64_t ACT_OF = 7ull | 4ull << 4 | 8ull << 8 | 3ull << 12 | 0ull << 16 | 1ull << 20 |
+                            6ull << 24 | 2ull << 28 | 5ull << 32;
 
-// One wave holds 64 / lw worlds, lw lanes each (lw = 16, 32 or 64; the host picks it
-// from N and the grid size).  A call is a chain of LDS round trips (move ->
-// post-move reads -> goal stamps -> stores), and the waves are too few to hide
-// them, so the chain is kept short: every LDS read a step needs is issued in one
-// batch (the move's cell and obstacle word, the observation cells of the next
-// step, the next-action probes, the agents), the visible-goals plane is a
-// per-call stamp (no clearing pass), and the next call's (id, action) is read
-// while this one runs.
-constexpr int PR_IT = 4;  // observation cells per lane held in registers (s*s <= 4 lw)
+// x / d for 0 <= x < 2^32 with m = ceil(2^48 / d)
+__device__ inline int fdiv(int x, uint64_t m) { return (int)(((uint64_t)(uint32_t)x * m) >> 48); }
 
-// S, LS: observation size and log2(lanes per world) fixed at compile time (0: from
-// QGeo).  PRIMAL's default observation_size (10, `:175`) gets specialised kernels:
-// the window walk and the planes' store offsets become immediates.
-template <int S, int LS>
+// S: observation size fixed at compile time (0: g.s); LS: log2(lanes per world);
+// DIAG: DIAGONAL_MOVEMENT; MA: agents per lane held in registers (>= g.apl).
+template <int S_, int LS, bool DIAG, int MA>
 __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
   extern __shared__ __align__(16) unsigned char lds[];
-  const int lws = LS ? LS : g.lw_shift;
-  const int lw = 1 << lws, lane = threadIdx.x;
-  const int wl = lane >> lws, ag = lane & (lw - 1), lead = wl << lws;
-  const int e = blockIdx.x * (64 >> lws) + wl;
+  constexpr int lw = 1 << LS;
+  constexpr int NDIR = DIAG ? 8 : 4;
+  const int lane = threadIdx.x, wl = lane >> LS, ag = lane & (lw - 1), lead = wl << LS;
+  const int e = blockIdx.x * (64 >> LS) + wl;
   const bool live = e < g.E;
   const uint64_t wmask = (lw == 64 ? ~0ull : ((1ull << lw) - 1ull)) << lead;
-  const int N = g.N, H = g.H, W = g.W, s = S ? S : g.s, ss = s * s;
+  const int N = g.N, H = g.H, W = g.W, P = g.P, PW = g.PW;
+  const int s = S_ ? S_ : g.s, ss = s * s, h2 = s / 2;
+  const int apl = MA == 1 ? 1 : g.apl;
   unsigned char* wr = lds + wl * g.wreg;
-  uint8_t* occ = wr;                                           // [H*W] 0 empty, id + 1
-  uint32_t* obst = (uint32_t*)(wr + ((g.hw + 15) & ~15));      // [bits_words]
-  int2* pos = (int2*)((unsigned char*)obst + ((g.bits_words * 4 + 15) & ~15));  // [N]
-  int2* gl = pos + N;                                          // [N]
-  int2* pend = gl + N;                                         // [64] goal vector (dx, dy) of a block's calls
-  int2* pairL = pend + 64;                                     // [64] a block's (agent id, action)
-  int* flag = (int*)(pairL + 64);                              // [4] move status
-  int* stamp = flag + 4;                                       // [s*s] call k + 1 marks a visible goal
+  uint8_t* cm = wr;                                   // [rows][PW] agent | wall << 1
+  const uint32_t* cm32 = (const uint32_t*)wr;
+  uint32_t* bm = (uint32_t*)(wr + g.off_bm);          // obstacle bitmap (set-up only)
+  uint8_t* gim = wr + g.off_goals;                    // [s*s] visible goals of the call
+  int4* agL = (int4*)(wr + g.off_ag);                 // [N] {row, col, goal row, goal col}
+  int2* pairL = (int2*)(wr + g.off_pair);             // [64] a block's (agent id, action)
+  int2* pend = (int2*)(wr + g.off_pend);              // [64] goal vector (dx, dy) of a block's calls
+  double* rst = (double*)(wr + g.off_rst);            // [64] rewards of a block's calls
+  uint8_t* fst = wr + g.off_fst;                      // [5][64] done, on_goal, valid, mask lo / hi
 
+  // ---- agents: lane ag owns agents ag + r * lw (registers) and their LDS records ----
+  int px[MA], py[MA], gx[MA], gy[MA], qx[MA], qy[MA];
+  bool has[MA];
+#pragma unroll
+  for (int r = 0; r < MA; ++r) {
+    const int b = ag + r * lw;
+    has[r] = live && r < apl && b < N;
+    px[r] = py[r] = gx[r] = gy[r] = qx[r] = qy[r] = -(1 << 20);  // far outside every window
+    if (has[r]) {
+      const long long i = (long long)e * N + b;
+      const int2 p = ((const int2*)a.pos)[i], q = ((const int2*)a.goal)[i];
+      px[r] = p.x, py[r] = p.y, gx[r] = q.x, gy[r] = q.y;
+      if constexpr (DIAG) {
+        const int2 pp = ((const int2*)a.past)[i];
+        qx[r] = pp.x, qy[r] = pp.y;
+      }
+      agL[b] = make_int4(p.x, p.y, q.x, q.y);
+    }
+  }
   if (live) {
-    for (int i = ag; i < g.hw; i += lw) occ[i] = 0;
-    for (int i = ag; i < ss; i += lw) stamp[i] = 0;
     const uint32_t* src = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)e * g.map_stride));
-    for (int w = ag; w < g.bits_words; w += lw) obst[w] = src[w];
-    for (int b = ag; b < N; b += lw) {
-      pos[b] = ((const int2*)a.pos)[(long long)e * N + b];
-      gl[b] = ((const int2*)a.goal)[(long long)e * N + b];
+    for (int w = ag; w < g.bits_words; w += lw) bm[w] = src[w];
+    for (int i = ag; i < (ss + 3) >> 2; i += lw) ((uint32_t*)gim)[i] = 0u;
+  }
+  wave_fence();
+  // ---- the padded map: 4 cells per dword, walls from the bitmap, border = wall ----
+  if (live) {
+    const int wpr = PW >> 2, nwd = g.rows * wpr;
+    for (int wi = ag; wi < nwd; wi += lw) {
+      const int pr = wi / wpr;
+      const int r = pr - P, c0 = (wi - pr * wpr) * 4 - P;
+      uint32_t v = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int c = c0 + t;
+        const bool in = r >= 0 && r < H && c >= 0 && c < W;
+        const int idx = in ? r * W + c : 0;
+        const bool wall = !in || ((bm[idx >> 5] >> (idx & 31)) & 1u);
+        v |= (wall ? 2u : 0u) << (8 * t);
+      }
+      ((uint32_t*)cm)[wi] = v;
     }
   }
   wave_fence();
-  if (live)
-    for (int b = ag; b < N; b += lw) occ[pos[b].x * W + pos[b].y] = (uint8_t)(b + 1);
+  int ngoal = 0;  // agents on their goal (State.done :159-166 is ngoal == N)
+#pragma unroll
+  for (int r = 0; r < MA; ++r) {
+    if (has[r]) cm[(px[r] + P) * PW + py[r] + P] = 1;  // agents start on free cells
+    ngoal += __popcll(__ballot(has[r] && px[r] == gx[r] && py[r] == gy[r]) & wmask);
+  }
   wave_fence();
-  // this lane's first observation cell (ag / s, ag % s) and the step to its next one
-  const int r_step = lw / s, c_step = lw % s;
-  const int r0 = ag / s, c0 = ag % s;
-  const bool probe = ag >= 1 && ag <= 4;  // lanes 1..4 test the next-action directions
+
+  // ---- per-lane constants of the observation planes (s even) ----
+  // lane m < s*s/4 writes cells 4m .. 4m+3 of each plane: nlow of them in window row
+  // y0 from column x0, the rest at the start of row y0 + 1 (o2; = o1 when none)
+  const bool even = (s & 1) == 0;
+  const int D = even ? ss >> 2 : ss;  // dwords a call writes per plane (even) / per record (odd)
+  constexpr int RW = 4;               // rounds held in registers (host: D <= 4 lw for even s)
+  int o1[RW], o2[RW];
+  uint32_t lom[RW];
+#pragma unroll
+  for (int rr = 0; rr < RW; ++rr) {
+    const int m = ag + rr * lw;
+    const int c4 = 4 * m, y0 = c4 / s, x0 = c4 - y0 * s, nlow = min(4, s - x0);
+    o1[rr] = y0 * PW + x0;
+    o2[rr] = nlow < 4 ? (y0 + 1) * PW + x0 - s : o1[rr];
+    lom[rr] = nlow >= 4 ? ~0u : (1u << (8 * nlow)) - 1u;
+  }
+  const bool probe = ag >= 1 && ag <= NDIR;
+  const int pofs = probe ? dir_r(ag) * PW + dir_c(ag) : 0;
 
   const long long e0k = (long long)e * a.K;
   int kstop = live ? a.K : 0;  // calls of this world from kstop on are not run (bad call)
@@ -135,129 +204,159 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
       const int aid = pa.x - 1, act = pa.y;
       pa = nxt;
       if (k >= kstop) continue;  // (uniform within a world)
-      const long long ek = e0k + k;
-      if (aid < 0 || aid >= N || act < 0 || act > 4) {  // the reference asserts (:556-558)
+      if (aid < 0 || aid >= N || act < 0 || act >= g.nact) {  // the reference asserts (:556-558)
         if (ag == 0 && a.err) atomicCAS(a.err, 0, e + 1);
         kstop = k;
         continue;
       }
-      // ---- State.moveAgent (:103-135), the world's first lane ----
-      if (ag == 0) {
-        const int2 p = pos[aid], gg = gl[aid];
-        const int nx = p.x + dir_r(act), ny = p.y + dir_c(act);
-        const bool inb = nx < H && nx >= 0 && ny < W && ny >= 0;
-        const int ci = inb ? nx * W + ny : 0;
-        const uint8_t oc = occ[ci];
-        const uint32_t ow = obst[ci >> 5];
-        // the status chain as selects (one branch, for the move's writes)
-        const bool on_old = gg.x == p.x && gg.y == p.y, on_new = gg.x == nx && gg.y == ny;
-        const bool wall = ((ow >> (ci & 31)) & 1u) != 0;
-        const bool moved = act != 0 && inb && oc == 0 && !wall;
-        const int st_move = on_new ? 1 : (on_old ? 2 : 0);
-        const int st_blocked = !inb ? -1 : (oc != 0 ? -3 : -2);  // robot before wall: state > 0
-        const int status = act == 0 ? (on_old ? 1 : 0) : (moved ? st_move : st_blocked);
-        if (moved) {
-          occ[p.x * W + p.y] = 0;
-          occ[ci] = (uint8_t)(aid + 1);
-          pos[aid] = make_int2(nx, ny);
+      // ---- State.moveAgent (:103-135), resolved by every lane of the world ----
+      const int4 A = agL[aid];  // broadcast read: aid's (row, col, goal row, goal col)
+      const int nx = A.x + dir_r(act), ny = A.y + dir_c(act);
+      const bool inb = nx < H && nx >= 0 && ny < W && ny >= 0;
+      const uint32_t tv = cm[(nx + P) * PW + ny + P];  // |d| <= 1 <= P: inside the padded map
+      bool dcol = false;
+      if constexpr (DIAG) {  // diagonalCollision (:77-99) against the PRE-move positions
+        const int sx = A.x + nx, sy = A.y + ny;
+        bool hit = false;
+#pragma unroll
+        for (int r = 0; r < MA; ++r)
+          hit |= has[r] && ag + r * lw != aid && qx[r] + px[r] == sx && qy[r] + py[r] == sy;
+        dcol = (__ballot(hit) & wmask) != 0;
+      }
+      const bool wall = (tv & 2u) != 0, robot = (tv & 1u) != 0;
+      const bool moved = act != 0 && inb && !wall && !robot && !dcol;
+      const bool on_old = A.z == A.x && A.w == A.y, on_new = A.z == nx && A.w == ny;
+      const int st_blocked = !inb ? -1 : (wall ? -2 : -3);  // out of bounds, wall, robot / diagonal
+      const int status = act == 0 ? (on_old ? 1 : 0) : (moved ? (on_new ? 1 : (on_old ? 2 : 0)) : st_blocked);
+      const int cx = moved ? nx : A.x, cy = moved ? ny : A.y;
+      ngoal += (moved && on_new ? 1 : 0) - (moved && on_old ? 1 : 0);
+      if (moved && ag == 0) {
+        cm[(A.x + P) * PW + A.y + P] = 0;
+        cm[(nx + P) * PW + ny + P] = 1;
+        *(int2*)&agL[aid] = make_int2(nx, ny);
+      }
+#pragma unroll
+      for (int r = 0; r < MA; ++r) {
+        if (ag + r * lw == aid) {
+          if constexpr (DIAG) {
+            if (act == 0 || moved) qx[r] = A.x, qy[r] = A.y;  // agents_past (:110-112, :129-131)
+          }
+          px[r] = cx, py[r] = cy;
         }
-        flag[0] = status;
       }
       wave_fence();
-      // ---- one batch of LDS reads on the post-move world ----
-      const int status = flag[0];
-      const int2 p = pos[aid], gg = gl[aid];
-      const int ax = p.x, ay = p.y;
-      const int tr = ax - s / 2, tc = ay - s / 2;
-      // _observe cells (:343-386) held in registers: occupant and obstacle word
-      uint8_t ocv[PR_IT];
-      uint32_t obv[PR_IT];
-      int cidx[PR_IT];  // map cell, -1 outside the map
-      {
-        int rr = r0, cc = c0;
+      // ---- _observe (:343-386) on the post-move world, next valid actions ----
+      const int tr = cx - h2, tc = cy - h2;
+      const int base = (tr + P) * PW + tc + P;  // first window cell in the padded map
+      const int gq = (A.z >= tr && A.z < tr + s && A.w >= tc && A.w < tc + s)
+                         ? (A.z - tr) * s + (A.w - tc) : -(1 << 20);  // own goal's window cell
+      uint32_t V[RW];
+      if (a.obs && even) {
 #pragma unroll
-        for (int it = 0; it < PR_IT; ++it) {
-          const int r = tr + rr, c = tc + cc;
-          const bool in = ag + it * lw < ss && r < H && r >= 0 && c < W && c >= 0;
-          cidx[it] = in ? r * W + c : -1;
-          const int ci = in ? r * W + c : 0;
-          ocv[it] = occ[ci];  // (unconditional: cell 0 when outside or no obs)
-          obv[it] = obst[ci >> 5];
-          rr += r_step;
-          cc += c_step;
-          if (cc >= s) {
-            cc -= s;
-            ++rr;
+        for (int rr = 0; rr < RW; ++rr) {
+          V[rr] = 0;
+          if (rr * lw < D && ag + rr * lw < D) {
+            const int A1 = base + o1[rr], A2 = base + o2[rr];
+            const uint32_t v1 = __builtin_amdgcn_alignbyte(cm32[(A1 >> 2) + 1], cm32[A1 >> 2], A1 & 3);
+            const uint32_t v2 = __builtin_amdgcn_alignbyte(cm32[(A2 >> 2) + 1], cm32[A2 >> 2], A2 & 3);
+            V[rr] = (v1 & lom[rr]) | (v2 & ~lom[rr]);
           }
         }
       }
-      // _listNextValidActions (:639-667): direction ag probed by lane ag of the world
-      bool ok = false;
-      if (probe) {
-        const int nx = ax + dir_r(ag), ny = ay + dir_c(ag);
-        const bool inb = nx < H && nx >= 0 && ny < W && ny >= 0;
-        const int ci = inb ? nx * W + ny : 0;
-        ok = inb && occ[ci] == 0 && !((obst[ci >> 5] >> (ci & 31)) & 1u);
-      }
-      // agents: done (:159-166) and visible agents' goals, clamped into view (:374-378)
-      bool off = false;
-      for (int b = ag; b < N; b += lw) {
-        const int2 pb = pos[b], gb = gl[b];
-        off |= (pb.x != gb.x) || (pb.y != gb.y);
-        if (a.obs && b != aid && pb.x >= tr && pb.x < tr + s && pb.y >= tc && pb.y < tc + s) {
-          const int mr = max(tr, min(tr + s - 1, gb.x));
-          const int mc = max(tc, min(tc + s - 1, gb.y));
-          stamp[(mr - tr) * s + (mc - tc)] = k + 1;
+      bool ok = false;  // _listNextValidActions (:639-667): lane d probes action d
+      if (probe) ok = cm[(cx + P) * PW + cy + P + pofs] == 0;  // in bounds, no wall, no robot
+      uint32_t dmask = 0;  // DIAG: directions refused by diagonalCollision from (cx, cy)
+#pragma unroll
+      for (int r = 0; r < MA; ++r) {
+        const int b = ag + r * lw;
+        if (a.obs && has[r] && b != aid && px[r] >= tr && px[r] < tr + s && py[r] >= tc && py[r] < tc + s) {
+          const int mr = max(tr, min(tr + s - 1, gx[r])), mc = max(tc, min(tc + s - 1, gy[r]));
+          gim[(mr - tr) * s + (mc - tc)] = 1;  // a visible agent's goal, clamped into view (:374-378)
+        }
+        if constexpr (DIAG) {
+          const int sx = qx[r] + px[r] - 2 * cx, sy = qy[r] + py[r] - 2 * cy;
+          if (has[r] && b != aid && sx >= -1 && sx <= 1 && sy >= -1 && sy <= 1)
+            dmask |= 1u << (uint32_t)((ACT_OF >> (4 * ((sx + 1) * 3 + sy + 1))) & 0xFu);
         }
       }
-      const bool done = (__ballot(off) & wmask) == 0;
-      const uint32_t mbits = (uint32_t)(__ballot(ok) >> lead) & 0x1Eu;  // bits 1..4 = actions
+      uint32_t mask = 1u | ((uint32_t)(__ballot(ok) >> lead) & (NDIR == 8 ? 0x1FEu : 0x1Eu));
+      if constexpr (DIAG) {
+#pragma unroll
+        for (int d = 1; d <= 8; ++d)
+          if (__ballot((dmask >> d) & 1u) & wmask) mask &= ~(1u << d);
+      }
+      const int opp = opposite(act);
+      if (opp > 0) mask &= ~(1u << opp);
       wave_fence();
       if (a.obs) {
-        uint8_t* o = a.obs + ek * 4 * ss;
-        const int gcell = gg.x * W + gg.y;
-        const auto cell = [&](int i, int ci, uint8_t oc, uint32_t ow) {  // branch-free selects
-          const bool in = ci >= 0, agent = oc != 0;
-          const bool wall = ((ow >> (ci & 31)) & 1u) != 0;
-          o[i] = (in && agent) ? 1 : 0;                   // :363-365, 369-372
-          o[ss + i] = ci == gcell ? 1 : 0;                // :366-368 (ci = -1 outside)
-          o[2 * ss + i] = stamp[i] == k + 1 ? 1 : 0;
-          o[3 * ss + i] = (!in || (!agent && wall)) ? 1 : 0;  // outside: obstacle (:356-362)
-        };
+        uint8_t* o = a.obs + (e0k + k) * 4 * ss;
+        if (even) {
 #pragma unroll
-        for (int it = 0; it < PR_IT; ++it) {
-          const int i = ag + it * lw;
-          if (i < ss) cell(i, cidx[it], ocv[it], obv[it]);
-        }
-        for (int i = ag + PR_IT * lw; i < ss; i += lw) {  // large windows: the rest
-          const int r = tr + i / s, c = tc + i % s;
-          const bool in = r < H && r >= 0 && c < W && c >= 0;
-          const int ci = in ? r * W + c : 0;
-          cell(i, in ? ci : -1, occ[ci], obst[ci >> 5]);
+          for (int rr = 0; rr < RW; ++rr) {
+            const int m = ag + rr * lw;
+            if (rr * lw < D && m < D) {
+              uint32_t* g32 = (uint32_t*)gim + m;
+              const uint32_t gw = *g32;
+              *g32 = 0u;  // clear for the next call (in order before its stamps)
+              const int d = gq - 4 * m;
+              const uint32_t g4 = (uint32_t)d < 4u ? 1u << (8 * d) : 0u;
+              uint32_t* o32 = (uint32_t*)(o + 4 * m);
+              o32[0] = V[rr] & 0x01010101u;              // poss: own and other agents (:363-372)
+              o32[ss >> 2] = g4;                         // goal (:366-368)
+              o32[ss >> 1] = gw;                         // goals of visible agents (:374-378)
+              o32[3 * (ss >> 2)] = (V[rr] >> 1) & 0x01010101u;  // obstacles, outside = 1 (:356-362)
+            }
+          }
+        } else {  // odd s: record dword m, byte by byte (plane = byte / s^2)
+          for (int m = ag; m < ss; m += lw) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              const int b = 4 * m + t;
+              const int pl = fdiv(b, g.m_ss), i = b - pl * ss;
+              const int y = fdiv(i, g.m_s), x = i - y * s;
+              const uint32_t v = cm[base + y * PW + x];
+              uint32_t bv;
+              if (pl == 0) bv = v & 1u;
+              else if (pl == 1) bv = i == gq ? 1u : 0u;
+              else if (pl == 2) {
+                bv = gim[i];
+                gim[i] = 0;
+              } else bv = (v >> 1) & 1u;
+              w |= bv << (8 * t);
+            }
+            ((uint32_t*)o)[m] = w;
+          }
         }
       }
       if (ag == 0) {
         // ---- reward (:579-596), JOINT = False; stay-on-goal blocking term = 0 ----
         const double rew = act == 0 ? (status == 1 ? GOAL_REWARD + 0 : IDLE_COST)
                                     : status == 1 ? GOAL_REWARD : status < 0 ? COLLISION_REWARD : ACTION_COST;
-        uint32_t m = 1u | mbits;
-        const int opp = act == 1 ? 3 : act == 2 ? 4 : act == 3 ? 1 : act == 4 ? 2 : -1;  // :26
-        if (opp > 0) m &= ~(1u << opp);
-        if (a.reward) a.reward[ek] = rew;
-        if (a.done) a.done[ek] = done ? 1 : 0;
-        if (a.next_mask) a.next_mask[ek] = (uint8_t)m;
-        if (a.on_goal) a.on_goal[ek] = (ax == gg.x && ay == gg.y) ? 1 : 0;
-        if (a.valid) a.valid[ek] = status >= 0 ? 1 : 0;
-        // goal vector (:379-384): its magnitude needs a LUT load, so the call's
-        // (dx, dy) waits in LDS and the world writes a block's vectors together
-        // (one load latency per 64 calls instead of one per call)
-        pend[k - kb] = make_int2(gg.x - ax, gg.y - ay);
+        const int j = k - kb;
+        rst[j] = rew;
+        fst[j] = ngoal == N ? 1 : 0;                          // world.done() (:626)
+        fst[64 + j] = (cx == A.z && cy == A.w) ? 1 : 0;       // on_goal (:633)
+        fst[128 + j] = status >= 0 ? 1 : 0;                   // valid_action (:566)
+        fst[192 + j] = (uint8_t)mask;
+        if constexpr (DIAG) fst[256 + j] = (uint8_t)(mask >> 8);
+        pend[j] = make_int2(A.z - cx, A.w - cy);              // goal vector (:379-384), LUT later
       }
-      wave_fence();
     }
-    if (a.vec) {  // the block's goal vectors, calls kb .. min(kend, kstop) - 1
-      const int n = min(kend, kstop) - kb;
-      for (int j = ag; j < n; j += lw) {
+    wave_fence();
+    // ---- the block's staged outputs, calls kb .. min(kend, kstop) - 1, as runs ----
+    const int n = min(kend, kstop) - kb;
+    const long long o0 = e0k + kb;
+    for (int j = ag; j < n; j += lw) {
+      if (a.reward) a.reward[o0 + j] = rst[j];
+      if (a.done) a.done[o0 + j] = fst[j];
+      if (a.on_goal) a.on_goal[o0 + j] = fst[64 + j];
+      if (a.valid) a.valid[o0 + j] = fst[128 + j];
+      if (a.next_mask) {
+        if constexpr (DIAG) ((uint16_t*)a.next_mask)[o0 + j] = (uint16_t)(fst[192 + j] | (fst[256 + j] << 8));
+        else a.next_mask[o0 + j] = fst[192 + j];
+      }
+      if (a.vec) {
         const int2 d = pend[j];
         const double mag = a.pow_lut[d.x * d.x + d.y * d.y];
         double vx = (double)d.x, vy = (double)d.y;
@@ -265,7 +364,7 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
           vx = vx / mag;
           vy = vy / mag;
         }
-        double* v = a.vec + (e0k + kb + j) * 3;
+        double* v = a.vec + (o0 + j) * 3;
         v[0] = vx;
         v[1] = vy;
         v[2] = mag;
@@ -273,8 +372,13 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
     }
     wave_fence();
   }
-  if (live)
-    for (int b = ag; b < N; b += lw) ((int2*)a.pos)[(long long)e * N + b] = pos[b];
+#pragma unroll
+  for (int r = 0; r < MA; ++r) {
+    if (!has[r]) continue;
+    const long long i = (long long)e * N + ag + r * lw;
+    ((int2*)a.pos)[i] = make_int2(px[r], py[r]);
+    if constexpr (DIAG) ((int2*)a.past)[i] = make_int2(qx[r], qy[r]);
+  }
 }
 
 int perr(int code, const char* msg) { return mapfx_internal_error(code, msg); }
@@ -296,6 +400,51 @@ struct mapfx_primal_t {
   int lds;
 };
 
+namespace {
+
+using PrimalFn = void (*)(QGeo, QArgs);
+
+template <int S, int LS, bool DIAG>
+PrimalFn pick_ma(int apl) {
+  if (apl <= 1) return primal_act_kernel<S, LS, DIAG, 1>;
+  return primal_act_kernel<S, LS, DIAG, 4>;
+}
+template <int S, bool DIAG>
+PrimalFn pick_ls(int ls, int apl) {
+  if (ls == 4) return pick_ma<S, 4, DIAG>(apl);
+  if (ls == 5) return pick_ma<S, 5, DIAG>(apl);
+  return pick_ma<S, 6, DIAG>(apl);
+}
+PrimalFn pick_primal(const QGeo& g) {
+  if (g.s == 10) return g.diag ? pick_ls<10, true>(g.lw_shift, g.apl) : pick_ls<10, false>(g.lw_shift, g.apl);
+  return g.diag ? pick_ls<0, true>(g.lw_shift, g.apl) : pick_ls<0, false>(g.lw_shift, g.apl);
+}
+
+uint64_t magic48(int d) { return ((1ull << 48) + (uint64_t)d - 1) / (uint64_t)d; }
+int r16(int x) { return (x + 15) & ~15; }
+
+// LDS layout of one world for lanes-per-world 1 << ls; returns its size.
+int layout(QGeo& g) {
+  int o = r16(g.rows * g.PW + 4);  // + the realigning read's overrun
+  g.off_bm = o;
+  o += r16(g.bits_words * 4);
+  g.off_goals = o;
+  o += r16(g.s * g.s + 4);
+  g.off_ag = o;
+  o += 16 * g.N;
+  g.off_pair = o;
+  o += 64 * 8;
+  g.off_pend = o;
+  o += 64 * 8;
+  g.off_rst = o;
+  o += 64 * 8;
+  g.off_fst = o;
+  o += 5 * 64;
+  return r16(o);
+}
+
+}  // namespace
+
 extern "C" {
 
 int mapfx_primal_create(const mapfx_primal_cfg* cfg, mapfx_primal_t** out) {
@@ -310,6 +459,7 @@ int mapfx_primal_create(const mapfx_primal_cfg* cfg, mapfx_primal_t** out) {
   mapfx_primal_t* h = new (std::nothrow) mapfx_primal_t();
   if (!h) return perr(MAPFX_ENOMEM, "host allocation failed");
   QGeo& g = h->geo;
+  memset(&g, 0, sizeof(g));
   g.H = c.H;
   g.W = c.W;
   g.N = c.n_agents;
@@ -320,24 +470,46 @@ int mapfx_primal_create(const mapfx_primal_cfg* cfg, mapfx_primal_t** out) {
   g.hw = c.H * c.W;
   g.bits_words = (g.hw + 31) / 32;
   g.lut_n = (c.H - 1) * (c.H - 1) + (c.W - 1) * (c.W - 1) + 1;
-  g.wreg = ((g.hw + 15) & ~15) + ((g.bits_words * 4 + 15) & ~15) + 16 * g.N + 64 * 8 + 64 * 8 + 16 +
-           ((4 * g.s * g.s + 15) & ~15);
-  // Lanes per world: the smallest of 16 / 32 / 64 that covers N, widened while the
-  // grid has fewer than 2 waves per SIMD (2048 waves) or the wave's worlds would
-  // pass 64 KB of LDS.  Packing worlds saves issue slots (the per-call work is
-  // mostly per world, not per cell), more waves hide the call's LDS chain; at
-  // 4096 worlds of N = 16 (the bench) 16 / 32 / 64 lanes measured 149 / 120 / 125 us
-  // per 64-call launch.
-  // MAPFX_PRIMAL_LANES (16 / 32 / 64) overrides the first two rules (tests).
-  g.lw_shift = g.N <= 16 ? 4 : g.N <= 32 ? 5 : 6;
+  g.diag = c.diagonal ? 1 : 0;
+  g.nact = g.diag ? 9 : 5;
+  g.P = std::max(1, g.s / 2);
+  g.PW = (c.W + 2 * g.P + 3) & ~3;
+  g.rows = c.H + 2 * g.P;
+  g.m_s = magic48(g.s);
+  g.m_ss = magic48(g.s * g.s);
+  const int wreg = layout(g);
+  // Lanes per world: the smallest of 16 / 32 / 64 that writes an even-s call's planes
+  // in at most 4 rounds (s * s / 4 dwords per plane) and holds the agents in at most
+  // 4 registers each, widened while the grid has fewer than 2 waves per SIMD (2048
+  // waves: more waves hide the call's LDS round trips) or a wave's worlds would pass
+  // 64 KB of LDS.  At 4096 worlds, s = 10 (the bench) this is 32 lanes, 2 worlds a
+  // wave.  MAPFX_PRIMAL_LANES (16 / 32 / 64) overrides the wave-count rule (tests).
+  const int D = (g.s % 2 == 0) ? g.s * g.s / 4 : 1;
+  int ls = 4;
+  while (ls < 6 && (D > 4 * (1 << ls) || g.N > 4 * (1 << ls))) ++ls;
   const char* force = getenv("MAPFX_PRIMAL_LANES");
   const int fl = force ? atoi(force) : 0;
-  if (fl == 16 || fl == 32 || fl == 64) g.lw_shift = std::max(g.lw_shift, fl == 16 ? 4 : fl == 32 ? 5 : 6);
+  if (fl == 16 || fl == 32 || fl == 64) ls = std::max(ls, fl == 16 ? 4 : fl == 32 ? 5 : 6);
   else
-    while (g.lw_shift < 6 && (long long)(g.E + (64 >> g.lw_shift) - 1) / (64 >> g.lw_shift) < 2048) ++g.lw_shift;
-  while (g.lw_shift < 6 && (64 >> g.lw_shift) * g.wreg > 65536) ++g.lw_shift;
-  g.lw = 1 << g.lw_shift;
-  h->lds = (64 >> g.lw_shift) * g.wreg;
+    while (ls < 6 && (long long)(g.E + (64 >> ls) - 1) / (64 >> ls) < 2048) ++ls;
+  while (ls < 6 && (64 >> ls) * wreg > 65536) ++ls;
+  if ((64 >> ls) * wreg > 160 * 1024) {
+    delete h;
+    return perr(MAPFX_EINVAL, "PRIMAL world needs too much LDS");
+  }
+  g.lw_shift = ls;
+  g.lw = 1 << ls;
+  g.apl = (g.N + g.lw - 1) / g.lw;
+  g.wreg = wreg;
+  h->lds = (64 >> ls) * wreg;
+  if (h->lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)pick_primal(g),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, h->lds);
+    if (e != hipSuccess) {
+      delete h;
+      return check_hip(e, "hipFuncSetAttribute");
+    }
+  }
   double* lut = (double*)malloc(sizeof(double) * g.lut_n);
   if (!lut) {
     delete h;
@@ -367,6 +539,7 @@ int mapfx_primal_act(mapfx_primal_t* h, const mapfx_primal_state* st, const int3
                      const int32_t* actions, int32_t K, const mapfx_primal_out* out, void* stream) {
   if (!h) return perr(MAPFX_EINVAL, "NULL handle");
   if (!st || !st->pos || !st->goal || !st->map_bits) return perr(MAPFX_EINVAL, "bad state");
+  if (h->geo.diag && !st->past) return perr(MAPFX_EINVAL, "diagonal movement needs state.past");
   if (K < 0) return perr(MAPFX_EINVAL, "K < 0");
   if (K == 0 || h->geo.E == 0) return MAPFX_OK;
   if (!agent_ids || !actions) return perr(MAPFX_EINVAL, "NULL agent_ids / actions");
@@ -375,6 +548,7 @@ int mapfx_primal_act(mapfx_primal_t* h, const mapfx_primal_state* st, const int3
   a.pos = st->pos;
   a.goal = st->goal;
   a.bits = st->map_bits;
+  a.past = st->past;
   a.ids = agent_ids;
   a.acts = actions;
   a.K = K;
@@ -389,14 +563,9 @@ int mapfx_primal_act(mapfx_primal_t* h, const mapfx_primal_state* st, const int3
     a.vec = out->vec;
     a.err = out->err;
   }
-  const int wpw = 64 >> h->geo.lw_shift;
-  const dim3 grid((h->geo.E + wpw - 1) / wpw), block(64);
-  const hipStream_t sm = (hipStream_t)stream;
   const QGeo& g = h->geo;
-  if (g.s == 10 && g.lw_shift == 4) hipLaunchKernelGGL((primal_act_kernel<10, 4>), grid, block, h->lds, sm, g, a);
-  else if (g.s == 10 && g.lw_shift == 5) hipLaunchKernelGGL((primal_act_kernel<10, 5>), grid, block, h->lds, sm, g, a);
-  else if (g.s == 10 && g.lw_shift == 6) hipLaunchKernelGGL((primal_act_kernel<10, 6>), grid, block, h->lds, sm, g, a);
-  else hipLaunchKernelGGL((primal_act_kernel<0, 0>), grid, block, h->lds, sm, g, a);
+  const int wpw = 64 >> g.lw_shift;
+  hipLaunchKernelGGL(pick_primal(g), dim3((g.E + wpw - 1) / wpw), dim3(64), h->lds, (hipStream_t)stream, g, a);
   return check_hip(hipGetLastError(), "primal_act_kernel launch");
 }
 

@@ -71,11 +71,12 @@ class POut(ctypes.Structure):
 
 
 class QCfg(ctypes.Structure):  # include/mapfx_primal.h
-    _fields_ = [(k, c_i32) for k in ("H", "W", "n_agents", "n_envs", "obs_size", "map_shared")]
+    _fields_ = [(k, c_i32) for k in ("H", "W", "n_agents", "n_envs", "obs_size", "map_shared",
+                                     "diagonal")]
 
 
 class QState(ctypes.Structure):
-    _fields_ = [(k, c_vp) for k in ("pos", "goal", "map_bits")]
+    _fields_ = [(k, c_vp) for k in ("pos", "goal", "map_bits", "past")]
 
 
 class QOut(ctypes.Structure):

@@ -27,7 +27,7 @@ class PrimalBatch:
     PRIMAL's world0) or `bits` [E|1, map_stride]; starts / goals [E, N, 2] (row, col)."""
 
     def __init__(self, starts, goals, grids=None, bits=None, hw=None, observation_size=10,
-                 device=None):
+                 device=None, diagonal=False, past=None):
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise RuntimeError("PrimalBatch runs on a HIP device only (got %s)" % self.device)
@@ -52,8 +52,10 @@ class PrimalBatch:
         self._check_placement(starts, goals, bits)
         self.map_shared = bits.shape[0] == 1 and self.E != 1
         self.s = int(observation_size)
+        self.diagonal = bool(diagonal)
+        self.n_actions = 9 if self.diagonal else 5
         cfg = _abi.QCfg(H=self.H, W=self.W, n_agents=self.N, n_envs=self.E, obs_size=self.s,
-                        map_shared=1 if self.map_shared else 0)
+                        map_shared=1 if self.map_shared else 0, diagonal=1 if self.diagonal else 0)
         with torch.cuda.device(self.device):
             h = ctypes.c_void_p()
             check(lib.mapfx_primal_create(ctypes.byref(cfg), ctypes.byref(h)), "mapfx_primal_create")
@@ -63,7 +65,13 @@ class PrimalBatch:
         self.pos = torch.as_tensor(starts).to(dev).contiguous()
         self.goal = torch.as_tensor(goals).to(dev).contiguous()
         self.err = torch.zeros((1,), dtype=torch.int32, device=dev)
-        self._state = _abi.QState(pos=ptr(self.pos), goal=ptr(self.goal), map_bits=ptr(self.bits))
+        # agents_past (DIAGONAL_MOVEMENT): equal to the starts in a fresh world (:55-66)
+        self.past = None
+        if self.diagonal:
+            pp = starts if past is None else np.array(past, dtype=np.int32)
+            self.past = torch.as_tensor(pp).to(dev).contiguous()
+        self._state = _abi.QState(pos=ptr(self.pos), goal=ptr(self.goal), map_bits=ptr(self.bits),
+                                  past=ptr(self.past))
         self._K = -1
         self.out = None
 
@@ -94,7 +102,8 @@ class PrimalBatch:
         E, s, dev = self.E, self.s, self.device
         z = lambda shape, dt: torch.zeros(shape, dtype=dt, device=dev)  # noqa: E731
         self.out = {"reward": z((E, K), torch.float64), "done": z((E, K), torch.uint8),
-                    "next_mask": z((E, K), torch.uint8), "on_goal": z((E, K), torch.uint8),
+                    "next_mask": z((E, K), torch.int16 if self.diagonal else torch.uint8),
+                    "on_goal": z((E, K), torch.uint8),
                     "valid": z((E, K), torch.uint8), "obs": z((E, K, 4, s, s), torch.uint8),
                     "vec": z((E, K, 3), torch.float64)}
         self._out = _abi.QOut(err=ptr(self.err), **{k: ptr(self.out[k]) for k in _OUT_KEYS})
@@ -137,8 +146,8 @@ class MAPFEnv:
     def __init__(self, num_agents=1, observation_size=10, world0=None, goals0=None,
                  DIAGONAL_MOVEMENT=False, SIZE=(10, 40), PROB=(0, .5), FULL_HELP=False,
                  blank_world=False, device=None):
-        if DIAGONAL_MOVEMENT:
-            raise NotImplementedError("DIAGONAL_MOVEMENT is not on the hot path")
+        self.DIAGONAL_MOVEMENT = bool(DIAGONAL_MOVEMENT)
+        self.n_actions = 9 if self.DIAGONAL_MOVEMENT else 5
         self.num_agents = int(num_agents)
         self.observation_size = int(observation_size)
         self.SIZE, self.PROB, self.FULL_HELP = SIZE, PROB, FULL_HELP
@@ -161,7 +170,8 @@ class MAPFEnv:
         self.initial_world, self.initial_goals = world0.copy(), goals0.copy()
         self._grid = np.where(world0 < 0, -1, 0).astype(np.int8)
         self.batch = PrimalBatch([starts], [goals], grids=self._grid,
-                                 observation_size=self.observation_size, device=self._device)
+                                 observation_size=self.observation_size, device=self._device,
+                                 diagonal=self.DIAGONAL_MOVEMENT)
         self.finished = False
         self.fresh = True
         self.individual_rewards = [0 for _ in range(self.num_agents)]
@@ -171,7 +181,8 @@ class MAPFEnv:
         self._set_world(world0, goals0)
         o = self.batch.act([[agent_id]], [[0]])  # a stay call changes nothing; it reports
         mask = int(o["next_mask"][0, 0].item())  # the valid moves with no previous action
-        return [a for a in range(5) if (mask >> a) & 1], bool(o["on_goal"][0, 0].item()), False
+        return ([a for a in range(self.n_actions) if (mask >> a) & 1],
+                bool(o["on_goal"][0, 0].item()), False)
 
     def getObstacleMap(self):
         return (self._grid == -1).astype(int)
@@ -185,7 +196,7 @@ class MAPFEnv:
     def _step(self, action_input, episode=0):
         """:549-637 -> (state, reward, done, nextActions, on_goal, blocking, valid)."""
         assert len(action_input) == 2, 'Action input should be a tuple with the form (agent_id, action)'
-        assert action_input[1] in range(5), 'Invalid action'
+        assert action_input[1] in range(self.n_actions), 'Invalid action'
         assert action_input[0] in range(1, self.num_agents + 1)
         agent_id, action = action_input
         o = self.batch.act([[agent_id]], [[action]])
@@ -196,7 +207,7 @@ class MAPFEnv:
         mask = int(o["next_mask"][0, 0].item())
         self.individual_rewards[agent_id - 1] = reward
         self.finished |= done
-        next_actions = [a for a in range(5) if (mask >> a) & 1]
+        next_actions = [a for a in range(self.n_actions) if (mask >> a) & 1]
         state = ([obs[i] for i in range(4)], vec)
         return (state, reward, done, next_actions, bool(o["on_goal"][0, 0].item()), False,
                 bool(o["valid"][0, 0].item()))

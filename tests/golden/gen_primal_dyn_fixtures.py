@@ -10,7 +10,9 @@ and records every call's outputs as .npz fixtures (`pd_*.npz`).
 The "stay on goal" reward adds get_blocking_reward (:513-546), which needs the
 un-vendored od_mstar3 planner: it is replaced by 0 on the instance here, so that
 term is "parity unpinned"  and the port defines it as 0.
-JOINT = False and DIAGONAL_MOVEMENT = False, the reference's defaults (:27, :175).
+JOINT = False (the reference's default, :27); DIAGONAL_MOVEMENT (:175) is False
+(the default) in the first four fixtures and True in `pd_diag_*` (actions 5..8,
+agents_past, State.diagonalCollision :77-99).
 
 Usage:  python tests/golden/gen_primal_dyn_fixtures.py
 """
@@ -28,25 +30,27 @@ PR = G.PR
 OUT_DIR = G.OUT_DIR
 
 
-def make_env(grid, starts, goals, size):
+def make_env(grid, starts, goals, size, diagonal=False):
     world = grid.astype(np.int64).copy()
     gg = np.zeros(grid.shape, dtype=np.int64)
     for a, ((r, c), (gr, gc)) in enumerate(zip(starts, goals)):
         world[r, c] = a + 1
         gg[gr, gc] = a + 1
-    env = PR.MAPFEnv(num_agents=len(starts), observation_size=size, world0=world, goals0=gg)
+    env = PR.MAPFEnv(num_agents=len(starts), observation_size=size, world0=world, goals0=gg,
+                     DIAGONAL_MOVEMENT=diagonal)
     env.get_blocking_reward = lambda agent_id: 0  # od_mstar3 absent: term unpinned, defined 0
     return env
 
 
-def run(name, grid, starts, goals, size, rounds, rng, script=None):
-    env = make_env(grid, starts, goals, size)
+def run(name, grid, starts, goals, size, rounds, rng, script=None, diagonal=False):
+    env = make_env(grid, starts, goals, size, diagonal)
     n = len(starts)
     calls = []
     if script is None:
-        script = [(a + 1, int(rng.integers(0, 5))) for _ in range(rounds) for a in range(n)]
+        script = [(a + 1, int(rng.integers(0, 9 if diagonal else 5)))
+                  for _ in range(rounds) for a in range(n)]
     rec = {k: [] for k in ("agent", "action", "reward", "done", "next_mask", "on_goal", "valid",
-                           "blocking", "pos", "obs", "vec")}
+                           "blocking", "pos", "obs", "vec", "past")}
     for aid, act in script:
         state, reward, done, nxt, on_goal, blocking, valid = env._step((aid, act))
         mask = 0
@@ -61,12 +65,14 @@ def run(name, grid, starts, goals, size, rounds, rng, script=None):
         rec["valid"].append(bool(valid))
         rec["blocking"].append(bool(blocking))
         rec["pos"].append(np.array(env.getPositions(), dtype=np.int32))
+        rec["past"].append(np.array(env.world.agents_past, dtype=np.int32))
         m, v = state
         rec["obs"].append(np.stack([np.asarray(x) for x in m]).astype(np.uint8))
         rec["vec"].append(np.array(v, dtype=np.float64))
         calls.append((aid, act))
     out = {"grid": grid.astype(np.int8), "starts": np.array(starts, dtype=np.int32),
-           "goals": np.array(goals, dtype=np.int32), "size": np.array(size)}
+           "goals": np.array(goals, dtype=np.int32), "size": np.array(size),
+           "diagonal": np.array(bool(diagonal))}
     for k, v in rec.items():
         out[k] = np.array(v)
     out["reward"] = out["reward"].astype(np.float64)
@@ -106,6 +112,31 @@ def main():
     cells = free_pick(rng, g, 40)
     order = [(int(a) + 1, int(rng.integers(0, 5))) for _ in range(12) for a in rng.permutation(20)]
     run("rand16_n20_perm", g, cells[:20], cells[20:], 9, 0, rng, script=order)
+    # --- DIAGONAL_MOVEMENT = True (actions 0..8) ---
+    rng = np.random.default_rng(1234)
+    # 5. 10x10 random obstacles, 8 agents, s = 10, 30 rounds of random actions 0..8
+    g = (rng.random((10, 10)) < 0.2).astype(np.int8) * -1
+    cells = free_pick(rng, g, 16)
+    run("diag_rand10_n8", g, cells[:8], cells[8:], 10, 30, rng, diagonal=True)
+    # 6. crowded 6x6, 14 agents, s = 5: many crossings of past moves
+    g = np.zeros((6, 6), dtype=np.int8)
+    g[0, 5] = -1
+    cells = free_pick(rng, g, 28)
+    run("diag_crowd6_n14", g, cells[:14], cells[14:], 5, 30, rng, diagonal=True)
+    # 7. scripted diagonal crossings: agent 1 (2,2) -> 5 (1,1) to (3,3); agent 2 at (2,3)
+    #    tries 6 (1,-1) to (3,2): same midpoint -> -3, also in agent 2's next-action mask;
+    #    a stay resets agents_past; the opposite of a diagonal move leaves the mask
+    g = np.zeros((6, 6), dtype=np.int8)
+    g[4, 4] = -1
+    starts, goals = [(2, 2), (2, 3), (0, 0)], [(5, 5), (5, 0), (0, 5)]
+    script = [(1, 5), (2, 6), (2, 0), (1, 0), (2, 6), (3, 5), (3, 8), (1, 7), (2, 5), (3, 6),
+              (1, 5), (1, 5), (2, 7), (3, 2), (2, 8), (1, 6), (3, 0), (2, 1)]
+    run("diag_script6", g, starts, goals, 4, 0, rng, script=script, diagonal=True)
+    # 8. 16x16, 20 agents, s = 7 (odd: the byte path), random order, actions 0..8
+    g = (rng.random((16, 16)) < 0.15).astype(np.int8) * -1
+    cells = free_pick(rng, g, 40)
+    order = [(int(a) + 1, int(rng.integers(0, 9))) for _ in range(10) for a in rng.permutation(20)]
+    run("diag_rand16_n20_perm", g, cells[:20], cells[20:], 7, 0, rng, script=order, diagonal=True)
 
 
 if __name__ == "__main__":

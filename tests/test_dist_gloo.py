@@ -183,7 +183,8 @@ class _OracleTrajBatch:
 
     def out_spec(self, T):
         E, N, W = self.E, self.N, self.W
-        return {"obs_window": ((T, E, N, 2, W, W), torch.int8), "reward": ((T, E), torch.float64),
+        return {"obs_window": ((T, E, N, 2, W, W), torch.int8),
+                "obs_window_occ": ((T, E, N, W, W), torch.int8), "reward": ((T, E), torch.float64),
                 "traj_done": ((T, E, N), torch.uint8), "traj_pos": ((T, E, N, 2), torch.int32)}
 
     def rollout(self, T, actions=None, seed=0, t0=0, traj=None, outputs=None):
@@ -195,6 +196,9 @@ class _OracleTrajBatch:
             o = self.ob.observe(window=self.W, full=False)
             traj["reward"][k].copy_(torch.from_numpy(r["reward"]))
             traj["obs_window"][k].copy_(torch.from_numpy(o["obs_window"]))
+            ob_, ag_ = o["obs_window"][:, :, 0], o["obs_window"][:, :, 1]   # -> occ = agents - obst
+            traj["obs_window_occ"][k].copy_(torch.from_numpy(np.where(ob_ == 1, -1, ag_)
+                                                             .astype(np.int8)))
             traj["traj_done"][k].copy_(torch.from_numpy(self.ob.done))
             traj["traj_pos"][k].copy_(torch.from_numpy(self.ob.pos))
         return traj
@@ -203,7 +207,7 @@ class _OracleTrajBatch:
 _OG = dict(S=12, N=6, W=5, T=3, chunks=3, E=5)
 
 
-def _og_worker(rank, world, port, q):
+def _og_worker(rank, world, port, q, keys):
     import sys
     sys.path[:0] = [REPO, PKG_ROOT]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -216,7 +220,7 @@ def _og_worker(rank, world, port, q):
         inst = synthetic_instances(c["E"], c["S"], c["S"], c["N"], p_obstacle=0.1, seed=5,
                                    env_offset=rank * c["E"])
         fb = _OracleTrajBatch(inst, c["S"], c["N"], c["W"], rank * c["E"])
-        og = OverlappedGather(fb, c["T"])
+        og = OverlappedGather(fb, c["T"], keys=keys)
         assert og.bytes_per_chunk() % 16 == 0
         got = []
         for i in range(c["chunks"]):
@@ -232,16 +236,21 @@ def _og_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_overlapped_gather_packed_world2():
+@pytest.mark.parametrize("keys", [("obs_window", "reward", "traj_done"),
+                                  ("obs_window_occ", "reward", "traj_done"),
+                                  ("reward", "traj_done")])
+def test_overlapped_gather_packed_world2(keys):
     """OverlappedGather at world 2 (gloo): ONE gather per chunk of the packed
-    (obs_window, reward, done) prefix, double-buffered receive side; rank 0's
-    per-chunk result equals an unsharded run, env for env."""
+    (obs, reward, done) prefix, double-buffered receive side; rank 0's per-chunk
+    result equals an unsharded run, env for env.  The payloads of bench.py
+    --gather-payload: the two window planes, the occupancy window (half the bytes,
+    the planes follow from it), or reward + done only."""
     from mapfx.maps import synthetic_instances
     world, c = 2, _OG
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_og_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_og_worker, args=(r, world, port, q, keys)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
@@ -254,7 +263,7 @@ def test_overlapped_gather_packed_world2():
         traj = {k: torch.zeros(s, dtype=d) for k, (s, d) in fb.out_spec(c["T"]).items()}
         fb.rollout(c["T"], seed=9, t0=i * c["T"], traj=traj)
         g = got[i]
-        assert set(g) == {"obs_window", "reward", "traj_done"}
+        assert set(g) == set(keys)
         for k in g:
             # [world, T, E_rank, ...] -> [T, world * E_rank, ...]
             merged = np.concatenate(list(g[k]), axis=1)

@@ -270,22 +270,30 @@ def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T, obs, win):
     (256, 1, 5, False, 16), (256, 2, 5, False, 16), (256, 3, 3, False, 16), (252, 17, 7, False, 16),
     (64, 40, 5, True, 16),
     (250, 12, 5, False, 12), (130, 9, 3, True, 7), (66, 10, 5, False, 40),  # N < L
-    (130, 12, 5, False, 64), (64, 40, 3, True, 64), (40, 9, 7, False, 64)])  # 64-agent store wave
+    (130, 12, 5, False, 64), (64, 40, 3, True, 64), (40, 9, 7, False, 64),  # 64-agent store wave
+    # obs_window_occ records from the store wave (the gather payload of bench --gpus N)
+    (4096, 20, 5, False, -16), (256, 3, 3, False, -16), (252, 17, 7, False, -16),
+    (64, 40, 5, True, -16)])
 def test_runner_rollout_every_step(mapfx_mod, E, T, win, autoreset, N):
     """Runner rollouts (every PyMARL output, no full map; N = 16 takes the store-wave
-    kernel): each step's outputs must equal one step launch's, step by step."""
+    kernel): each step's outputs must equal one step launch's, step by step.
+    N < 0: the occupancy window (obs_window_occ) instead of the two planes; the
+    single steps write it with the generic kernel, the rollout with the store wave."""
     from mapfx.maps import synthetic_instances
+    occ = N < 0
+    N = abs(N)
+    wkey = "obs_window_occ" if occ else "obs_window"
     S = 32 if not autoreset else (8 if N <= 16 else 12)
     inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=12)
     kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=2000 if not autoreset else 9,
-              obs=("window",), window=win)
+              obs=("window_occ",) if occ else ("window",), window=win)
     b1 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
     b2 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
     b1.reset()
     b2.reset()
     acts = b2.gen_actions(T, 21, t0=0)
     traj = b1.rollout(T, actions=acts, autoreset=autoreset)
-    keys = ("reward", "reward_f32", "term", "node", "edge", "avail", "obs_window")
+    keys = ("reward", "reward_f32", "term", "node", "edge", "avail", wkey)
     for k in range(T):
         out = b2.step(acts[k])
         for key in keys:

@@ -40,8 +40,9 @@ def test_primal_matches_reference_goldens(mapfx_mod, name, chunk):
     """All calls in one launch (chunk 0) or split over launches of `chunk` calls:
     the world state carries over between launches."""
     fx = _load(name)
+    diag = bool(fx.get("diagonal", False))
     b = mapfx_mod.PrimalBatch(fx["starts"][None], fx["goals"][None], grids=fx["grid"][None],
-                              observation_size=int(fx["size"]))
+                              observation_size=int(fx["size"]), diagonal=diag)
     n = len(fx["agent"])
     step = n if chunk == 0 else chunk
     for k0 in range(0, n, step):
@@ -56,19 +57,22 @@ def test_primal_matches_reference_goldens(mapfx_mod, name, chunk):
         assert np.array_equal(_np(o["obs"])[0], fx["obs"][sl])
         assert np.array_equal(_np(o["vec"])[0].view(np.uint64), fx["vec"][sl].view(np.uint64))
         assert np.array_equal(_np(b.pos)[0], fx["pos"][k1 - 1])
+        if diag:
+            assert np.array_equal(_np(b.past)[0], fx["past"][k1 - 1])
     b.check_err()
 
 
-def test_primal_dropin_matches_reference_goldens(mapfx_mod):
+@pytest.mark.parametrize("name", ["pd_script5", "pd_diag_script6"])
+def test_primal_dropin_matches_reference_goldens(mapfx_mod, name):
     from mapfx.primal import MAPFEnv
-    fx = _load("pd_script5")
+    fx = _load(name)
     world = fx["grid"].astype(np.int64)
     gg = np.zeros_like(world)
     for a, ((r, c), (gr, gc)) in enumerate(zip(fx["starts"], fx["goals"])):
         world[r, c] = a + 1
         gg[gr, gc] = a + 1
     env = MAPFEnv(num_agents=len(fx["starts"]), observation_size=int(fx["size"]), world0=world,
-                  goals0=gg)
+                  goals0=gg, DIAGONAL_MOVEMENT=bool(fx["diagonal"]))
     for k in range(len(fx["agent"])):
         (maps, vec), r, done, nxt, on_goal, blocking, valid = env._step(
             (int(fx["agent"][k]), int(fx["action"][k])))
@@ -95,6 +99,7 @@ def _random_worlds(rng, E, H, W, N, density, shared):
     return grids, starts, goals
 
 
+@pytest.mark.parametrize("diag", [False, True])
 @pytest.mark.parametrize("lanes", ["", "16", "32"])  # host's choice (64 at E = 64) / packed lane groups
 @pytest.mark.parametrize("H,W,N,s,K,shared,density", [
     (12, 12, 10, 7, 60, False, 0.2),
@@ -105,21 +110,25 @@ def _random_worlds(rng, E, H, W, N, density, shared):
     (32, 32, 16, 10, 70, False, 0.1),     # observation_size 10 (the default): specialised kernels
     (15, 17, 40, 10, 66, True, 0.1),      # s = 10 at 64 lanes (N > 32)
 ])
-def test_primal_batch_matches_oracle(mapfx_mod, monkeypatch, lanes, H, W, N, s, K, shared, density):
+def test_primal_batch_matches_oracle(mapfx_mod, monkeypatch, lanes, H, W, N, s, K, shared, density,
+                                    diag):
     from oracle.primal_dyn_oracle import PrimalWorld
     monkeypatch.setenv("MAPFX_PRIMAL_LANES", lanes)
-    rng = np.random.default_rng(H * 1000 + N)
+    rng = np.random.default_rng(H * 1000 + N + (7 if diag else 0))
     E = 64
     grids, starts, goals = _random_worlds(rng, E, H, W, N, density, shared)
     ids = rng.integers(1, N + 1, size=(E, K)).astype(np.int32)
-    # bias toward moves (1..4); some stays
-    acts = rng.choice(5, size=(E, K), p=[0.1, 0.225, 0.225, 0.225, 0.225]).astype(np.int32)
-    b = mapfx_mod.PrimalBatch(starts, goals, grids=grids, observation_size=s)
+    # bias toward moves; some stays
+    if diag:
+        acts = rng.choice(9, size=(E, K), p=[0.04] + [0.12] * 8).astype(np.int32)
+    else:
+        acts = rng.choice(5, size=(E, K), p=[0.1, 0.225, 0.225, 0.225, 0.225]).astype(np.int32)
+    b = mapfx_mod.PrimalBatch(starts, goals, grids=grids, observation_size=s, diagonal=diag)
     o = {k: _np(v).copy() for k, v in b.act(ids, acts).items()}
     pos = _np(b.pos)
     b.check_err()
     for e in list(range(0, E, 16)) + [E - 1]:
-        w = PrimalWorld(grids[0 if shared else e], starts[e], goals[e], s)
+        w = PrimalWorld(grids[0 if shared else e], starts[e], goals[e], s, diagonal=diag)
         for k in range(K):
             maps, vec, r, done, mask, on_goal, _, valid = w.step(int(ids[e, k]) - 1, int(acts[e, k]))
             assert np.float64(r).view(np.uint64) == o["reward"][e, k].view(np.uint64), (e, k)
@@ -128,6 +137,8 @@ def test_primal_batch_matches_oracle(mapfx_mod, monkeypatch, lanes, H, W, N, s, 
             assert np.array_equal(maps, o["obs"][e, k]), (e, k)
             assert np.array_equal(vec.view(np.uint64), o["vec"][e, k].view(np.uint64)), (e, k)
         assert np.array_equal(np.array(w.pos), pos[e]), e
+        if diag:
+            assert np.array_equal(np.array(w.past), _np(b.past)[e]), e
 
 
 @pytest.mark.parametrize("N", [3, 20, 40])  # 16, 32 and 64 lanes per world (forced)
@@ -181,6 +192,20 @@ def test_primal_bad_call_sets_err(mapfx_mod):
     b.act([[1], [1]], [[0], [5]])  # action 5 (diagonal) not available
     with pytest.raises(AssertionError, match="world 1"):
         b.check_err()
+
+
+def test_primal_diagonal_action_range(mapfx_mod):
+    """DIAGONAL_MOVEMENT: actions 5..8 are moves, 9 is refused (:552-557)."""
+    g = np.zeros((5, 5), np.int8)
+    b = mapfx_mod.PrimalBatch([[[2, 2]], [[0, 0]]], [[[4, 4]], [[1, 1]]], grids=g[None],
+                              observation_size=3, diagonal=True)
+    o = b.act([[1, 1], [1, 1]], [[5, 7], [5, 9]])    # world 1, call 1: action 9 is invalid
+    with pytest.raises(AssertionError, match="world 1"):
+        b.check_err()
+    assert _np(b.pos).tolist() == [[[2, 2]], [[1, 1]]]  # world 0: (2,2) -> (3,3) -> (2,2)
+    assert _np(b.past).tolist() == [[[3, 3]], [[0, 0]]]
+    assert _np(o["valid"])[0].tolist() == [1, 1] and _np(o["on_goal"])[1, 0] == 1
+    assert o["next_mask"].dtype == torch.int16 and int(_np(o["next_mask"])[0, 0]) & (1 << 7) == 0
 
 
 def test_primal_rejects_bad_placement(mapfx_mod):

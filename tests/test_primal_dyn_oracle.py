@@ -16,7 +16,8 @@ def test_primal_dyn_oracle_matches_reference(name):
     from oracle.primal_dyn_oracle import PrimalWorld
     with np.load(os.path.join(GOLDEN, name + ".npz")) as z:
         fx = {k: z[k] for k in z.files}
-    w = PrimalWorld(fx["grid"], fx["starts"], fx["goals"], int(fx["size"]))
+    diag = bool(fx.get("diagonal", False))
+    w = PrimalWorld(fx["grid"], fx["starts"], fx["goals"], int(fx["size"]), diagonal=diag)
     for k in range(len(fx["agent"])):
         maps, vec, r, done, mask, on_goal, blocking, valid = w.step(int(fx["agent"][k]) - 1,
                                                                     int(fx["action"][k]))
@@ -26,5 +27,7 @@ def test_primal_dyn_oracle_matches_reference(name):
         assert on_goal == bool(fx["on_goal"][k]), k
         assert valid == bool(fx["valid"][k]), k
         assert np.array_equal(np.array(w.pos), fx["pos"][k]), k
+        if "past" in fx:   # agents_past (moves and stays update it; DIAGONAL_MOVEMENT reads it)
+            assert np.array_equal(np.array(w.past), fx["past"][k]), k
         assert np.array_equal(maps, fx["obs"][k]), k
         assert np.array_equal(vec.view(np.uint64), fx["vec"][k].view(np.uint64)), k

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r03a
 mkdir -p $OUT
 echo "[$(date +%T)] gpu tests"
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > $OUT/gpu_tests.txt 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.txt 2>&1
 rc=$?; tail -5 $OUT/gpu_tests.txt
 if [ $rc -ne 0 ]; then exit $rc; fi
 echo "[$(date +%T)] bench c2"

@@ -20,8 +20,10 @@
  * mapfx_last_error().  Not restated (out of scope): the `output`
  * mode's random collision repair (:262-275) and the visualisation hooks.
  *
- * Limits: N <= 64 (the step keeps one env in one wavefront), H, W <= 256 (one env's
- * LDS maps within the CU's 160 KB; maps wider than 64 take the multi-wave BFS).
+ * Limits: N <= 1024, H <= 1024, W <= 1536 (every map the reference ships, up to
+ * orz900d's 656 x 1491).  N <= 64 with H, W <= 256 keeps each env in one wavefront
+ * with its cell maps in LDS; otherwise one workgroup steps an env with the agents'
+ * cells in an LDS hash table and the obstacle bitmap read from HBM.
  */
 #ifndef MAPFX_PARTIAL_H
 #define MAPFX_PARTIAL_H
@@ -36,7 +38,7 @@ extern "C" {
 
 typedef struct mapfx_partial_cfg {
   int32_t H, W;             /* grid rows, cols                                      */
-  int32_t n_agents;         /* N <= 64                                              */
+  int32_t n_agents;         /* N <= 1024                                            */
   int32_t n_envs;           /* E (this rank's shard)                                */
   int64_t env_offset;       /* global id of env 0                                   */
   int32_t episode_limit;    /* :33                                                  */
@@ -67,9 +69,10 @@ typedef struct mapfx_partial_state {
   uint8_t* terminated;      /* [E] _terminated                                      */
   int32_t* total_coll;      /* [E] _total_number_collisions                         */
   const uint8_t* map_bits;  /* [E or 1][mapfx_map_stride(H, W)]                     */
-  int16_t* goal_dist;       /* [E][N][H*W] shortest-path lengths to each goal (-1:
+  void* goal_dist;          /* [E][N][H*W] shortest-path lengths to each goal (-1:
                                obstacle / unreachable), filled by
-                               mapfx_partial_goal_dist                              */
+                               mapfx_partial_goal_dist; int16, or int32 when H*W >
+                               32767 (mapfx_partial_goal_dist_elem_size)            */
 } mapfx_partial_state;
 
 /* Per-call outputs (device, caller-owned; NULL = not produced). */
@@ -87,6 +90,8 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out_han
 void mapfx_partial_destroy(mapfx_partial_t* h);
 /* 2*W*W + 13*K (:377 get_obs_size) */
 int32_t mapfx_partial_obs_dim(const mapfx_partial_t* h);
+/* 2 or 4: bytes per goal_dist entry (a path on H*W cells is shorter than H*W). */
+int32_t mapfx_partial_goal_dist_elem_size(int32_t H, int32_t W);
 
 /* BFS distance tables of every (masked) env's goals (:906-928: A* lengths on
  * the 4-connected free-cell graph == BFS levels). */

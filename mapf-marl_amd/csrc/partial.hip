@@ -15,7 +15,9 @@
 // Layout: one wavefront holds EPW envs (L = pow2ceil(N) lanes per env, lane =
 // agent); an env's padded cell map (c = count + 1 - obstacle, c == 0 blocked /
 // border) and its dep map (bit 7: obstacle, bits 0-6: the occupant's move) live in
-// LDS for the launch; state round-trips HBM between calls.  Every fp64 value is
+// LDS for the launch; state round-trips HBM between calls.  N > 64 or a side > 256
+// (the reference's larger maps and agent counts) take partial_wg_kernel: one
+// workgroup per env, the agents' cells in an LDS hash table, the map in HBM.  Every fp64 value is
 // computed in the reference's operation order; sqrt(int) and the completion bonus
 // come from host-libm LUTs (math.sqrt / float ** int are correctly rounded there).
 #include <hip/hip_runtime.h>
@@ -53,6 +55,9 @@ struct PGeo {
   int win, K, D, limit, hw;          // window, knn, obs dim, episode limit, H*W
   double move_rew, stay_rew, stay_goal_rew, nc_rew, ec_rew, env_rew;
   int sq_max, bonus_len;             // LUT sizes
+  int gd32;                          // goal-distance tables are int32 (H * W > 32767), else int16
+  int big;                           // workgroup-per-env path (N > 64 or H, W > 256), map in HBM
+  int hs_log, wg_lds, huge_lds;      // its LDS hash size (log2), block LDS; huge-map BFS LDS
 };
 
 struct PArgs {
@@ -69,7 +74,7 @@ struct PArgs {
   uint8_t* terminated;
   int32_t* total_coll;
   const uint8_t* bits;
-  const int16_t* gd;
+  const void* gd;  // int16 or int32 (g.gd32)
   const void* actions;
   int act_dtype;
   int do_step;       // 0: observe only
@@ -109,14 +114,22 @@ __device__ inline void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// goal distance of cell `cell` in agent `oa`'s table (int16, or int32 when H * W > 32767:
+// a path can be longer than 32767 cells there)
+__device__ __forceinline__ int goal_dist_at(const PGeo& g, const void* gd, long long oa, int cell) {
+  const long long i = oa * g.hw + cell;
+  return g.gd32 ? ((const int32_t*)gd)[i] : (int)((const int16_t*)gd)[i];
+}
+
 // ---------------------------------------------------------------------------
 // BFS distance tables: one wave per (env, agent), lane r holds row r of the grid
 // as a 64-bit mask; each level expands the frontier by shifts (same row) and
 // shuffles (rows r-1, r+1).  Distances go to LDS then out, row-major int16.
 // ---------------------------------------------------------------------------
+template <typename DT>
 __global__ void __launch_bounds__(64) partial_bfs_kernel(PGeo g, const uint8_t* bits,
                                                          const int32_t* goal, const uint8_t* mask,
-                                                         int16_t* gd) {
+                                                         DT* gd) {
   __shared__ int16_t dist[64 * 64];
   const int pair = blockIdx.x;  // env * N + agent
   const int env = pair / g.N;
@@ -154,8 +167,8 @@ __global__ void __launch_bounds__(64) partial_bfs_kernel(PGeo g, const uint8_t* 
     front = nxt;
   }
   wave_fence();
-  int16_t* out = gd + (long long)pair * g.hw;
-  for (int i = r; i < g.hw; i += 64) out[i] = dist[i];
+  DT* out = gd + (long long)pair * g.hw;
+  for (int i = r; i < g.hw; i += 64) out[i] = (DT)dist[i];
 }
 
 // Maps wider or taller than 64 (up to 256 x 256): one 256-thread workgroup per
@@ -163,16 +176,17 @@ __global__ void __launch_bounds__(64) partial_bfs_kernel(PGeo g, const uint8_t* 
 // exchanged through LDS (double-buffered, one barrier per level), distances go
 // straight to the table in global memory (its cells were set to -1 first).
 constexpr int BIGW = 4;  // 64-bit words per row: W <= 256
+template <typename DT>
 __global__ void __launch_bounds__(256) partial_bfs_big_kernel(PGeo g, const uint8_t* bits,
                                                               const int32_t* goal, const uint8_t* mask,
-                                                              int16_t* gd) {
+                                                              DT* gd) {
   __shared__ uint64_t front[2][256][BIGW];
   const int pair = blockIdx.x;  // env * N + agent
   const int env = pair / g.N;
   if (mask && !mask[env]) return;  // uniform per block
   const int r = threadIdx.x;
   const int H = g.H, W = g.W;
-  int16_t* out = gd + (long long)pair * g.hw;
+  DT* out = gd + (long long)pair * g.hw;
   uint64_t freem[BIGW], seen[BIGW], cur[BIGW];
 #pragma unroll
   for (int k = 0; k < BIGW; ++k) freem[k] = seen[k] = cur[k] = 0;
@@ -218,10 +232,466 @@ __global__ void __launch_bounds__(256) partial_bfs_big_kernel(PGeo g, const uint
       cur[k] = nxt[k];
       front[buf ^ 1][r][k] = nxt[k];
       mine |= nxt[k] != 0;
-      for (uint64_t m = nxt[k]; m; m &= m - 1) out[r * W + 64 * k + __builtin_ctzll(m)] = (int16_t)level;
+      for (uint64_t m = nxt[k]; m; m &= m - 1) out[r * W + 64 * k + __builtin_ctzll(m)] = (DT)level;
     }
     buf ^= 1;
     any = __syncthreads_or(mine ? 1 : 0) != 0;
+  }
+}
+
+// Maps larger than 256 on a side (the reference ships brc202d 481 x 530, orz900d
+// 656 x 1491, w_woundedcoast 578 x 642, ...): one 512-thread workgroup per (env,
+// agent), thread t owns rows t and t + 512 (H <= 1024), each row as up to 24 64-bit
+// words (W <= 1536).  The frontier rows live in LDS (H x words x 8 bytes: 126 KB for
+// orz900d); every thread keeps its rows' "free and not yet reached" masks and the
+// next frontier in registers, so a level is one LDS read phase, a barrier, one
+// write phase and the termination test.  Grid graphs are bipartite and unweighted:
+// level-synchronous expansion gives exactly the A* / BFS path lengths (:906-928).
+constexpr int HUGE_WORDS = 24;
+constexpr int HUGE_THREADS = 512;
+template <typename DT>
+__global__ void __launch_bounds__(HUGE_THREADS) partial_bfs_huge_kernel(PGeo g, const uint8_t* bits,
+                                                                        const int32_t* goal,
+                                                                        const uint8_t* mask, DT* gd) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  uint64_t* front = (uint64_t*)lds;  // [H][WW]
+  const int pair = blockIdx.x;       // env * N + agent
+  const int env = pair / g.N;
+  if (mask && !mask[env]) return;    // uniform per block
+  const int tid = threadIdx.x;
+  const int H = g.H, W = g.W, WW = (W + 63) >> 6;
+  DT* out = gd + (long long)pair * g.hw;
+  const uint64_t* b64 = (const uint64_t*)(bits + (g.map_shared ? 0 : (long long)env * g.map_stride));
+  const long long nb64 = (g.map_stride + 7) / 8;  // whole u64 words of one env's bitmap
+  for (int i = tid; i < g.hw; i += HUGE_THREADS) out[i] = (DT)-1;
+  for (int i = tid; i < H * WW; i += HUGE_THREADS) front[i] = 0ull;
+  uint64_t allow[2][HUGE_WORDS];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r = tid + j * HUGE_THREADS;
+#pragma unroll
+    for (int k = 0; k < HUGE_WORDS; ++k) {
+      allow[j][k] = 0ull;
+      if (r < H && k < WW) {  // bits r*W + 64k .. of the bitmap, 1 = obstacle
+        const long long p = (long long)r * W + 64 * k;
+        const long long wi = p >> 6;
+        const int sh = (int)(p & 63);
+        const uint64_t lo = b64[wi];
+        const uint64_t hi = (sh && wi + 1 < nb64) ? b64[wi + 1] : 0ull;
+        const uint64_t word = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+        const int nc = min(64, W - 64 * k);
+        const uint64_t cols = nc == 64 ? ~0ull : ((1ull << nc) - 1ull);
+        allow[j][k] = ~word & cols;
+      }
+    }
+  }
+  __syncthreads();  // the -1 fill and the zeroed frontier come first
+  const int gr = goal[2 * pair], gc = goal[2 * pair + 1];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    if (tid + j * HUGE_THREADS == gr) {
+#pragma unroll
+      for (int k = 0; k < HUGE_WORDS; ++k) {
+        if (k == (gc >> 6) && ((allow[j][k] >> (gc & 63)) & 1ull)) {
+          allow[j][k] &= ~(1ull << (gc & 63));
+          front[gr * WW + k] = 1ull << (gc & 63);
+          out[gr * W + gc] = (DT)0;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  int level = 0;
+  bool any = true;
+  while (any) {
+    ++level;
+    uint64_t nxt[2][HUGE_WORDS];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = tid + j * HUGE_THREADS;
+#pragma unroll
+      for (int k = 0; k < HUGE_WORDS; ++k) {
+        nxt[j][k] = 0ull;
+        if (r < H && k < WW) {
+          const uint64_t* fr = front + r * WW;
+          const uint64_t cur = fr[k];
+          const uint64_t lft = (cur << 1) | (k > 0 ? fr[k - 1] >> 63 : 0ull);
+          const uint64_t rgt = (cur >> 1) | (k + 1 < WW ? fr[k + 1] << 63 : 0ull);
+          const uint64_t up = r > 0 ? fr[k - WW] : 0ull;
+          const uint64_t dn = r + 1 < H ? fr[k + WW] : 0ull;
+          nxt[j][k] = (lft | rgt | up | dn) & allow[j][k];
+        }
+      }
+    }
+    __syncthreads();  // every read of this level's frontier is done
+    bool mine = false;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = tid + j * HUGE_THREADS;
+#pragma unroll
+      for (int k = 0; k < HUGE_WORDS; ++k) {
+        if (r < H && k < WW) {
+          front[r * WW + k] = nxt[j][k];
+          allow[j][k] &= ~nxt[j][k];
+          mine |= nxt[j][k] != 0ull;
+          for (uint64_t m = nxt[j][k]; m; m &= m - 1) out[r * W + 64 * k + __builtin_ctzll(m)] = (DT)level;
+        }
+      }
+    }
+    any = __syncthreads_or(mine ? 1 : 0) != 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Workgroup-per-env step for what the wave kernel cannot hold: N > 64 agents or a
+// side > 256 cells (SURVEY.md §8(f) F1 at the reference's full range).  One
+// 256-thread workgroup per env, thread t owns agents t, t + 256, ... (APL <= 4:
+// N <= 1024).  No dense map in LDS: the obstacle bitmap is read from HBM and the
+// agents' cells live in an LDS hash table (open addressing, keys = row * W + col,
+// >= 4 slots per agent) carrying per cell the PRE-step count, the POST-step count
+// and the move of a single pre-step occupant (the edge test's fast case), rebuilt
+// every launch.  Same operation order as partial_kernel for every fp64 value.
+// ---------------------------------------------------------------------------
+constexpr int WG_THREADS = 256;
+constexpr uint32_t HEMPTY = 0xFFFFFFFFu;
+constexpr uint32_t HPRE = 1u, HPOST = 1u << 11, HDEP_SH = 22;  // val = pre | post << 11 | dep << 22
+
+__device__ __forceinline__ uint32_t hslot0(uint32_t key, int hs_log) {
+  return (key * 0x9E3779B1u) >> (32 - hs_log);
+}
+// the slot of `key`, inserted if absent
+__device__ __forceinline__ int hinsert(uint32_t* keys, int hs_log, uint32_t key) {
+  const uint32_t msk = (1u << hs_log) - 1u;
+  uint32_t s = hslot0(key, hs_log);
+  while (true) {
+    const uint32_t k = keys[s];
+    if (k == key) return (int)s;
+    if (k == HEMPTY) {
+      const uint32_t old = atomicCAS(&keys[s], HEMPTY, key);
+      if (old == HEMPTY || old == key) return (int)s;
+    }
+    s = (s + 1) & msk;
+  }
+}
+// the value of `key` (0 when absent); all insertions done
+__device__ __forceinline__ uint32_t hlookup(const uint32_t* keys, const uint32_t* vals, int hs_log, uint32_t key) {
+  const uint32_t msk = (1u << hs_log) - 1u;
+  uint32_t s = hslot0(key, hs_log);
+  while (true) {
+    const uint32_t k = keys[s];
+    if (k == key) return vals[s];
+    if (k == HEMPTY) return 0u;
+    s = (s + 1) & msk;
+  }
+}
+
+template <int WIN, int APL>
+__global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  constexpr int H2 = WIN / 2, WW = WIN * WIN;
+  const int tid = threadIdx.x, env = blockIdx.x, N = g.N, H = g.H, W = g.W;
+  const int hs = 1 << g.hs_log;
+  uint32_t* keys = (uint32_t*)lds;                    // [hs]
+  uint32_t* vals = keys + hs;                         // [hs]
+  int* oldL = (int*)(vals + hs);                      // [N] pre-step cell (edge scan)
+  int* newL = oldL + N;                               // [N] post-step cell
+  int2* posL = (int2*)(newL + N);                     // [N] post-step (row, col) (KNN)
+  float* feat = (float*)(posL + N);                   // [N][FR]
+  double* rewL = (double*)(((uintptr_t)(feat + N * FR) + 15) & ~(uintptr_t)15);  // [N]
+  int* red = (int*)(rewL + N);                        // [8] block reductions
+  const uint8_t* bm = a.bits + (g.map_shared ? 0 : (long long)env * g.map_stride);
+  const auto obstacle = [&](int rr, int cc) {  // 1 outside the grid or on a static obstacle
+    if (rr < 0 || rr >= H || cc < 0 || cc >= W) return 1u;
+    const int idx = rr * W + cc;
+    return (uint32_t)((bm[idx >> 3] >> (idx & 7)) & 1u);
+  };
+
+  int r[APL], c[APL], gr[APL], gc[APL], ir[APL], ic[APL], steps[APL], gcost[APL], edge[APL];
+  bool has[APL], at_goal[APL], dn[APL];
+  uint32_t node[APL];
+  const bool reset_me = a.do_reset && (!a.reset_mask || a.reset_mask[env]);
+  int tcur = a.t[env], total = a.total_coll[env];
+  bool term = a.terminated[env] != 0;
+  if (reset_me) {
+    tcur = 0;
+    term = false;
+    total = 0;
+  }
+#pragma unroll
+  for (int k = 0; k < APL; ++k) {
+    const int ag = tid + k * WG_THREADS;
+    has[k] = ag < N;
+    r[k] = c[k] = gr[k] = gc[k] = ir[k] = ic[k] = steps[k] = edge[k] = 0;
+    gcost[k] = -1;
+    at_goal[k] = dn[k] = false;
+    node[k] = 0;
+    if (has[k]) {
+      const long long oa = (long long)env * N + ag;
+      const int2 q = ((const int2*)a.goal)[oa], ip = ((const int2*)a.init_pos)[oa];
+      gr[k] = q.x, gc[k] = q.y, ir[k] = ip.x, ic[k] = ip.y;
+      if (reset_me) {  // :125-163
+        r[k] = ir[k], c[k] = ic[k];
+      } else {
+        const int2 p = ((const int2*)a.pos)[oa];
+        r[k] = p.x, c[k] = p.y;
+        steps[k] = a.steps[oa];
+        at_goal[k] = a.at_goal[oa] != 0;
+        dn[k] = a.done[oa] != 0;
+        gcost[k] = a.goal_cost[oa];
+        node[k] = a.node[oa];
+        edge[k] = a.edge[oa];
+      }
+    }
+  }
+  for (int i = tid; i < hs; i += WG_THREADS) {
+    keys[i] = HEMPTY;
+    vals[i] = 0u;
+  }
+  if (tid < 8) red[tid] = 0;
+  __syncthreads();
+  // pre-step counts (the move test reads the PRE-step occupancy, :508-512)
+  int oslot[APL];
+#pragma unroll
+  for (int k = 0; k < APL; ++k) {
+    oslot[k] = 0;
+    if (has[k]) {
+      oslot[k] = hinsert(keys, g.hs_log, (uint32_t)(r[k] * W + c[k]));
+      atomicAdd(&vals[oslot[k]], HPRE);
+    }
+  }
+  __syncthreads();
+
+  // ---- step (:165-310) ----
+  int act[APL];
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < APL; ++k) {
+    act[k] = 4;
+    if (a.do_step && has[k]) {
+      act[k] = load_act(a.actions, a.act_dtype, (long long)env * N + tid + k * WG_THREADS);
+      if (act[k] < 0 || act[k] > 4) bad = true;
+    }
+  }
+  const bool skip = a.do_step && __syncthreads_or(bad ? 1 : 0) != 0;  // the reference asserts (:174)
+  if (a.do_step && !skip) {
+    ++tcur;  // :178
+    double rew[APL];
+    bool moved[APL];
+    int pre[APL], nr[APL], ncol[APL];
+    uint32_t dnew[APL];
+#pragma unroll
+    for (int k = 0; k < APL; ++k) {
+      rew[k] = 0.0;  // rewards[i] = 0 (:183)
+      moved[k] = false;
+      pre[k] = 0;
+      nr[k] = r[k], ncol[k] = c[k];
+      if (has[k] && !dn[k]) {  // :193-211
+        ++steps[k];
+        bool envc = false;
+        if (act[k] != 4) {
+          const int tr = r[k] + (act[k] == 0 ? -1 : act[k] == 1 ? 1 : 0);
+          const int tc = c[k] + (act[k] == 2 ? -1 : act[k] == 3 ? 1 : 0);
+          const bool out = tr < 0 || tr >= H || tc < 0 || tc >= W;
+          const int cnt = out ? 0 : (int)(hlookup(keys, vals, g.hs_log, (uint32_t)(tr * W + tc)) & 0x7FFu);
+          if (out || (obstacle(tr, tc) && cnt == 0)) envc = true;  // obstacle nobody stands on
+          else {
+            nr[k] = tr, ncol[k] = tc;
+            moved[k] = true;
+            pre[k] = cnt;
+          }
+        }
+        if (envc) rew[k] = rew[k] + g.env_rew;                          // :203
+        if (act[k] != 4) rew[k] = rew[k] + g.move_rew;                  // :207
+        else rew[k] = rew[k] + (at_goal[k] ? g.stay_goal_rew : g.stay_rew);  // :209-212
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < APL; ++k) {
+      if (!has[k]) continue;
+      const int ag = tid + k * WG_THREADS;
+      at_goal[k] = nr[k] == gr[k] && ncol[k] == gc[k];  // :214-219
+      if (at_goal[k]) gcost[k] = tcur;
+      if (tcur >= g.limit) {  // :221-225
+        term = true;
+        dn[k] = true;
+      }
+      const long long oa = (long long)env * N + ag;
+      const int opd = goal_dist_at(g, a.gd, oa, r[k] * W + c[k]);  // :227-233
+      const int npd = goal_dist_at(g, a.gd, oa, nr[k] * W + ncol[k]);
+      rew[k] = rew[k] + (double)(opd - npd) / (double)g.limit;
+      // the single pre-step occupant's move (0..3, 7: stayed) and the post-step count
+      atomicOr(&vals[oslot[k]], (moved[k] ? (uint32_t)act[k] : 7u) << HDEP_SH);
+      const int ns = hinsert(keys, g.hs_log, (uint32_t)(nr[k] * W + ncol[k]));
+      atomicAdd(&vals[ns], HPOST);
+      oldL[ag] = r[k] * W + c[k];
+      newL[ag] = nr[k] * W + ncol[k];
+    }
+    __syncthreads();
+    // node / edge collisions (:708-727, :822-857); total += (sum(node) + sum(edge)) // 2 (:239)
+    int esum = 0;
+#pragma unroll
+    for (int k = 0; k < APL; ++k) {
+      dnew[k] = 0u;
+      if (!has[k]) continue;
+      const uint32_t v = hlookup(keys, vals, g.hs_log, (uint32_t)(nr[k] * W + ncol[k]));
+      node[k] = ((v >> 11) & 0x7FFu) >= 2u ? 1u : 0u;
+      edge[k] = 0;
+      if (moved[k] && pre[k] > 0) {
+        if (pre[k] == 1) {
+          edge[k] = (int)((v >> HDEP_SH) & 7u) == (act[k] ^ 1) ? 1 : 0;
+        } else {
+          const int oc = r[k] * W + c[k], nc = nr[k] * W + ncol[k];
+          for (int j = 0; j < N; ++j) edge[k] += (oldL[j] == nc) & (newL[j] == oc);
+        }
+      }
+      esum += (int)node[k] + edge[k];
+    }
+    if (esum) atomicAdd(&red[0], esum);
+    int nat = 0;
+#pragma unroll
+    for (int k = 0; k < APL; ++k) nat += (has[k] && at_goal[k]) ? 1 : 0;
+    if (nat) atomicAdd(&red[1], nat);
+    __syncthreads();
+    total += red[0] / 2;
+    const bool all_at = red[1] == N;  // :283-299
+#pragma unroll
+    for (int k = 0; k < APL; ++k) {
+      if (!has[k]) continue;
+      rew[k] = rew[k] + g.nc_rew * (double)node[k];  // :247
+      rew[k] = rew[k] + g.ec_rew * (double)edge[k];  // :249
+      if (all_at) {
+        dn[k] = true;
+        rew[k] = rew[k] + a.bonus_lut[min(tcur, g.bonus_len - 1)];
+      }
+      rewL[tid + k * WG_THREADS] = rew[k];
+      r[k] = nr[k], c[k] = ncol[k];
+    }
+    if (all_at) term = true;
+    __syncthreads();
+    if (tid == 0) {  // sum(rewards): naive left fold in agent order (:310)
+      double R = 0.0;
+      for (int j = 0; j < N; ++j) R = R + rewL[j];
+      if (a.reward) a.reward[env] = R;
+    }
+  } else if (a.do_step && tid == 0) {
+    if (a.err) atomicCAS(a.err, 0, env + 1);
+    if (a.reward) a.reward[env] = 0.0;
+  }
+  __syncthreads();
+  // post-step occupancy: rebuild the table from the current cells (the step's post
+  // counts hold it already; a reset / observe pass counts the positions here)
+  if (!(a.do_step && !skip)) {
+    for (int i = tid; i < hs; i += WG_THREADS) {
+      keys[i] = HEMPTY;
+      vals[i] = 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < APL; ++k)
+      if (has[k]) atomicAdd(&vals[hinsert(keys, g.hs_log, (uint32_t)(r[k] * W + c[k]))], HPOST);
+  }
+  // ---- observations of the current state (:312-391) ----
+#pragma unroll
+  for (int k = 0; k < APL; ++k) {
+    if (!has[k]) continue;
+    const int ag = tid + k * WG_THREADS;
+    const int d0 = gr[k] - r[k], d1 = gc[k] - c[k];
+    const double nrm = a.sqrt_lut[d0 * d0 + d1 * d1];        // :937
+    const double ux = nrm == 0.0 ? 0.0 : (double)d0 / nrm;   // :938-941
+    const double uy = nrm == 0.0 ? 0.0 : (double)d1 / nrm;
+    float* fr = feat + ag * FR;
+    fr[0] = (float)r[k]; fr[1] = (float)c[k]; fr[2] = (float)ir[k]; fr[3] = (float)ic[k];
+    fr[4] = (float)gr[k]; fr[5] = (float)gc[k]; fr[6] = (float)ux; fr[7] = (float)uy;
+    fr[8] = (float)nrm; fr[9] = (float)node[k]; fr[10] = (float)edge[k]; fr[11] = (float)steps[k];
+    posL[ag] = make_int2(r[k], c[k]);
+  }
+  int gsum = 0;
+#pragma unroll
+  for (int k = 0; k < APL; ++k) gsum += has[k] ? gcost[k] : 0;
+  if (tid == 0) red[2] = 0;
+  __syncthreads();
+  if (gsum) atomicAdd(&red[2], gsum);
+  float* const env_obs = obs_env(a, env, g.D, N);
+  // the c value of a cell: count + 1 - obstacle, 0 = outside / an obstacle nobody stands on
+  const auto cval = [&](int rr, int cc) -> uint32_t {
+    if (rr < 0 || rr >= H || cc < 0 || cc >= W) return 0u;
+    const uint32_t cnt = (hlookup(keys, vals, g.hs_log, (uint32_t)(rr * W + cc)) >> 11) & 0x7FFu;
+    return cnt + 1u - obstacle(rr, cc);
+  };
+#pragma unroll
+  for (int k = 0; k < APL; ++k) {
+    if (!has[k]) continue;
+    const int ag = tid + k * WG_THREADS;
+    if (env_obs) {
+      float* o = env_obs + (long long)ag * g.D;
+      if constexpr (WIN > 0) {  // window planes (:327-342): OOB / obstacle -> 1; agents -> count
+        for (int y = 0; y < WIN; ++y)
+          for (int x = 0; x < WIN; ++x) {
+            const uint32_t cv = cval(r[k] + y - H2, c[k] + x - H2);
+            o[y * WIN + x] = cv == 0 ? 1.0f : 0.0f;
+            o[WW + y * WIN + x] = cv == 0 ? 0.0f : (float)(cv - 1u);
+          }
+      }
+      // K nearest agents (:346-372): self first, then the k-1 nearest others by L2
+      // distance (sorted() is stable: ties by agent index); rows past min(N, K) = -1
+      float* kn = o + 2 * WW;
+      const int K = g.K, km1 = min(N, K) - 1;
+      for (int q = 0; q < 11; ++q) kn[q] = feat[ag * FR + q];
+      kn[11] = (float)(H * W);  // distance to itself (:543-545)
+      kn[12] = feat[ag * FR + 11];
+      long long prev = -1;
+      for (int sI = 1; sI <= km1; ++sI) {
+        long long best = 0x7FFFFFFFFFFFFFFFll;
+        for (int j = 0; j < N; ++j) {
+          if (j == ag) continue;
+          const int2 pj = posL[j];
+          const int dr = r[k] - pj.x, dc = c[k] - pj.y;
+          const long long key = (long long)(dr * dr + dc * dc) * 1024 + j;
+          if (key > prev && key < best) best = key;
+        }
+        prev = best;
+        const int j = (int)(best & 1023);
+        const int sq = (int)(best >> 10);
+        float* row = kn + sI * NF;
+        for (int q = 0; q < 11; ++q) row[q] = feat[j * FR + q];
+        row[11] = (float)a.sqrt_lut[sq];
+        row[12] = feat[j * FR + 11];
+      }
+      for (int sI = km1 + 1; sI < K; ++sI)
+        for (int q = 0; q < NF; ++q) kn[sI * NF + q] = -1.0f;
+    }
+    if (a.avail) {  // avail (:399-433): neighbour in bounds and not a free-standing obstacle
+      uint32_t m = 16u;
+      if (cval(r[k] - 1, c[k])) m |= 1u;
+      if (cval(r[k] + 1, c[k])) m |= 2u;
+      if (cval(r[k], c[k] - 1)) m |= 4u;
+      if (cval(r[k], c[k] + 1)) m |= 8u;
+      a.avail[(long long)env * N + ag] = (uint8_t)m;
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && a.state) {  // state (:377-387): [total collisions, step count, sum(each goal cost)]
+    a.state[3 * env + 0] = (float)total;
+    a.state[3 * env + 1] = (float)tcur;
+    a.state[3 * env + 2] = (float)red[2];
+  }
+  // ---- state write-back ----
+#pragma unroll
+  for (int k = 0; k < APL; ++k) {
+    if (!has[k]) continue;
+    const long long oa = (long long)env * N + tid + k * WG_THREADS;
+    ((int2*)a.pos)[oa] = make_int2(r[k], c[k]);
+    a.steps[oa] = steps[k];
+    a.at_goal[oa] = at_goal[k] ? 1 : 0;
+    a.done[oa] = dn[k] ? 1 : 0;
+    a.goal_cost[oa] = gcost[k];
+    a.node[oa] = (uint8_t)node[k];
+    a.edge[oa] = edge[k];
+  }
+  if (tid == 0) {
+    a.t[env] = tcur;
+    a.terminated[env] = term ? 1 : 0;
+    a.total_coll[env] = total;
   }
 }
 
@@ -366,9 +836,8 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
         dn = true;
       }
       if (has) {                                            // :227-233
-        const int16_t* gdt = a.gd + oa * g.hw;
-        const int opd = gdt[r * g.W + c];
-        const int npd = gdt[nr * g.W + ncol];
+        const int opd = goal_dist_at(g, a.gd, oa, r * g.W + c);
+        const int npd = goal_dist_at(g, a.gd, oa, nr * g.W + ncol);
         rew = rew + (double)(opd - npd) / (double)g.limit;
       }
       // counts move; node / edge collisions (:708-727, :822-857)
@@ -704,11 +1173,38 @@ int check_state(const mapfx_partial_t* h, const mapfx_partial_state* st) {
   return MAPFX_OK;
 }
 
+template <int WIN>
+void (*pick_wg_apl(int apl))(PGeo, PArgs) {
+  if (apl <= 1) return partial_wg_kernel<WIN, 1>;
+  if (apl <= 2) return partial_wg_kernel<WIN, 2>;
+  return partial_wg_kernel<WIN, 4>;
+}
+
+void (*pick_wg(int win, int apl))(PGeo, PArgs) {
+  switch (win) {
+    case 0: return pick_wg_apl<0>(apl);
+    case 1: return pick_wg_apl<1>(apl);
+    case 3: return pick_wg_apl<3>(apl);
+    case 5: return pick_wg_apl<5>(apl);
+    case 7: return pick_wg_apl<7>(apl);
+    case 9: return pick_wg_apl<9>(apl);
+  }
+  return nullptr;
+}
+
+int wg_apl(const PGeo& g) { return (g.N + WG_THREADS - 1) / WG_THREADS; }
+
 int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
   const PGeo& g = h->geo;
   if (g.E == 0) return MAPFX_OK;
   a.sqrt_lut = h->sqrt_lut;
   a.bonus_lut = h->bonus_lut;
+  if (g.big) {  // N > 64 or a side > 256: one workgroup per env, map in HBM
+    void (*fn)(PGeo, PArgs) = pick_wg(g.win, wg_apl(g));
+    if (!fn) return perr(MAPFX_EINVAL, "obs_window must be one of 0, 1, 3, 5, 7, 9");
+    hipLaunchKernelGGL(fn, dim3(g.E), dim3(WG_THREADS), g.wg_lds, (hipStream_t)stream, g, a);
+    return check_hip(hipGetLastError(), "partial_wg_kernel launch");
+  }
   const int blocks = (g.E + g.EPW - 1) / g.EPW;
   void (*fn)(PGeo, PArgs) = nullptr;
   if (g.K == 5 && g.win == 5 && g.L == 16) fn = partial_kernel<5, 5, 16>;
@@ -763,9 +1259,9 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   if (!cfg || !out) return perr(MAPFX_EINVAL, "NULL argument");
   *out = nullptr;
   const mapfx_partial_cfg& c = *cfg;
-  if (c.H < 1 || c.W < 1 || c.H > 256 || c.W > 256)
-    return perr(MAPFX_EINVAL, "MARL_PARTIAL path supports 1 <= H, W <= 256");
-  if (c.n_agents < 1 || c.n_agents > 64) return perr(MAPFX_EINVAL, "n_agents must be in 1..64");
+  if (c.H < 1 || c.W < 1 || c.H > HUGE_THREADS * 2 || c.W > 64 * HUGE_WORDS)
+    return perr(MAPFX_EINVAL, "MARL_PARTIAL path supports 1 <= H <= 1024, 1 <= W <= 1536");
+  if (c.n_agents < 1 || c.n_agents > 4 * WG_THREADS) return perr(MAPFX_EINVAL, "n_agents must be in 1..1024");
   if (c.n_envs < 0) return perr(MAPFX_EINVAL, "n_envs < 0");
   if (c.episode_limit < 1) return perr(MAPFX_EINVAL, "episode_limit must be >= 1");
   if (c.obs_knn_agents < 1) return perr(MAPFX_EINVAL, "obs_knn_agents must be >= 1");
@@ -804,6 +1300,12 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.bits_env_bytes = round_up(g.bits_words * 4 + 4, 16);
   g.feat_env_bytes = round_up(64 * FR * 4, 16);
   g.rew_env_bytes = 64 * 8;
+  g.gd32 = (long long)c.H * c.W > 32767 ? 1 : 0;  // a path is shorter than H * W cells
+  g.big = (g.N > 64 || c.H > 256 || c.W > 256) ? 1 : 0;
+  g.hs_log = 8;
+  while ((1 << g.hs_log) < 4 * g.N) ++g.hs_log;
+  g.wg_lds = (1 << g.hs_log) * 8 + g.N * (4 + 4 + 8 + FR * 4) + 16 + g.N * 8 + 8 * 4;
+  g.huge_lds = (c.H > 256 || c.W > 256) ? c.H * ((c.W + 63) / 64) * 8 : 0;
   g.move_rew = c.move_reward;
   g.stay_rew = c.stay_reward;
   g.stay_goal_rew = c.stay_goal_reward;
@@ -813,12 +1315,17 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   const int per_env = 2 * g.map_env_bytes + g.bits_env_bytes + g.feat_env_bytes + 64 * 8 +
                       g.rew_env_bytes;
   // envs per wave: as many as fit 64 KB of LDS; one env may take up to the CU's
-  // 160 KB (maps up to 256 x 256), with the dynamic-LDS limit raised below
-  int EPW = 64 / L;
+  // 160 KB (maps up to 256 x 256), with the dynamic-LDS limit raised below (the
+  // workgroup path keeps no map in LDS)
+  int EPW = g.big ? 1 : 64 / L;
   while (EPW > 1 && EPW * per_env > 64 * 1024) --EPW;
-  if (EPW * per_env > 160 * 1024) {
+  if (!g.big && EPW * per_env > 160 * 1024) {
     delete h;
     return perr(MAPFX_EINVAL, "one env needs more than 160 KB of LDS (map too large)");
+  }
+  if (g.big && (g.wg_lds > 160 * 1024 || g.huge_lds > 160 * 1024)) {
+    delete h;
+    return perr(MAPFX_EINVAL, "MARL_PARTIAL: the workgroup path needs more than 160 KB of LDS");
   }
   g.EPW = EPW;
   int off = 0;
@@ -848,7 +1355,22 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
     }
   }
   g.lds = off;
-  if (g.lds > 64 * 1024) {
+  if (g.big) {
+    int rc0 = MAPFX_OK;
+    if (g.wg_lds > 64 * 1024)
+      rc0 = check_hip(hipFuncSetAttribute((const void*)pick_wg(g.win, wg_apl(g)),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, g.wg_lds),
+                      "hipFuncSetAttribute(partial_wg_kernel LDS)");
+    if (!rc0 && g.huge_lds > 64 * 1024)
+      rc0 = check_hip(hipFuncSetAttribute(g.gd32 ? (const void*)partial_bfs_huge_kernel<int32_t>
+                                                 : (const void*)partial_bfs_huge_kernel<int16_t>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, g.huge_lds),
+                      "hipFuncSetAttribute(partial_bfs_huge_kernel LDS)");
+    if (rc0) {
+      delete h;
+      return rc0;
+    }
+  } else if (g.lds > 64 * 1024) {
     int rc0 = MAPFX_OK;
     for (auto fn : {partial_kernel<5, 5, 16>, partial_kernel<5, 5, 8>, partial_kernel<5, 5, 32>,
                     partial_kernel<3, 5, 16>, partial_kernel<7, 5, 16>, partial_kernel<0, 0, 0>,
@@ -901,6 +1423,10 @@ void mapfx_partial_destroy(mapfx_partial_t* h) {
 
 int32_t mapfx_partial_obs_dim(const mapfx_partial_t* h) { return h ? h->geo.D : -1; }
 
+int32_t mapfx_partial_goal_dist_elem_size(int32_t H, int32_t W) {
+  return (long long)H * W > 32767 ? 4 : 2;
+}
+
 int mapfx_partial_goal_dist(mapfx_partial_t* h, const mapfx_partial_state* st,
                             const uint8_t* env_mask, void* stream) {
   if (!h) return perr(MAPFX_EINVAL, "NULL handle");
@@ -908,12 +1434,30 @@ int mapfx_partial_goal_dist(mapfx_partial_t* h, const mapfx_partial_state* st,
   if (rc) return rc;
   const PGeo& g = h->geo;
   if ((long long)g.E * g.N == 0) return MAPFX_OK;
-  if (g.H <= 64 && g.W <= 64)
-    hipLaunchKernelGGL(partial_bfs_kernel, dim3(g.E * g.N), dim3(64), 0, (hipStream_t)stream, g,
-                       st->map_bits, st->goal, env_mask, st->goal_dist);
-  else
-    hipLaunchKernelGGL(partial_bfs_big_kernel, dim3(g.E * g.N), dim3(256), 0, (hipStream_t)stream, g,
-                       st->map_bits, st->goal, env_mask, st->goal_dist);
+  const hipStream_t sm = (hipStream_t)stream;
+  const dim3 grid((unsigned)(g.E * g.N));
+  if (g.huge_lds) {
+    if (g.gd32)
+      hipLaunchKernelGGL(partial_bfs_huge_kernel<int32_t>, grid, dim3(HUGE_THREADS), g.huge_lds, sm, g,
+                         st->map_bits, st->goal, env_mask, (int32_t*)st->goal_dist);
+    else
+      hipLaunchKernelGGL(partial_bfs_huge_kernel<int16_t>, grid, dim3(HUGE_THREADS), g.huge_lds, sm, g,
+                         st->map_bits, st->goal, env_mask, (int16_t*)st->goal_dist);
+  } else if (g.H <= 64 && g.W <= 64) {
+    if (g.gd32)  // (not reached: 64 x 64 < 32768 cells)
+      hipLaunchKernelGGL(partial_bfs_kernel<int32_t>, grid, dim3(64), 0, sm, g, st->map_bits, st->goal,
+                         env_mask, (int32_t*)st->goal_dist);
+    else
+      hipLaunchKernelGGL(partial_bfs_kernel<int16_t>, grid, dim3(64), 0, sm, g, st->map_bits, st->goal,
+                         env_mask, (int16_t*)st->goal_dist);
+  } else {
+    if (g.gd32)
+      hipLaunchKernelGGL(partial_bfs_big_kernel<int32_t>, grid, dim3(256), 0, sm, g, st->map_bits,
+                         st->goal, env_mask, (int32_t*)st->goal_dist);
+    else
+      hipLaunchKernelGGL(partial_bfs_big_kernel<int16_t>, grid, dim3(256), 0, sm, g, st->map_bits,
+                         st->goal, env_mask, (int16_t*)st->goal_dist);
+  }
   return check_hip(hipGetLastError(), "partial_bfs_kernel launch");
 }
 

@@ -91,6 +91,7 @@ EXPORTS = ("mapfx_abi_version", "mapfx_last_error", "mapfx_map_stride", "mapfx_o
            "mapfx_create", "mapfx_destroy", "mapfx_query", "mapfx_reset", "mapfx_step",
            "mapfx_observe", "mapfx_rollout", "mapfx_rollout_timed", "mapfx_gen_actions", "mapfx_action",
            "mapfx_partial_create", "mapfx_partial_destroy", "mapfx_partial_obs_dim",
+           "mapfx_partial_goal_dist_elem_size",
            "mapfx_partial_goal_dist", "mapfx_partial_reset", "mapfx_partial_step",
            "mapfx_partial_observe", "mapfx_primal_create", "mapfx_primal_destroy",
            "mapfx_primal_act", "mapfx_runner_begin", "mapfx_runner_actions", "mapfx_runner_post",
@@ -143,6 +144,7 @@ def _load():
         "mapfx_partial_create": (c_i32, [P(PCfg), P(c_vp)]),
         "mapfx_partial_destroy": (None, [c_vp]),
         "mapfx_partial_obs_dim": (c_i32, [c_vp]),
+        "mapfx_partial_goal_dist_elem_size": (c_i32, [c_i32, c_i32]),
         "mapfx_partial_goal_dist": (c_i32, [c_vp, P(PState), c_vp, c_vp]),
         "mapfx_partial_reset": (c_i32, [c_vp, P(PState), c_vp, P(POut), c_vp]),
         "mapfx_partial_step": (c_i32, [c_vp, P(PState), c_vp, c_i32, P(POut), c_vp]),

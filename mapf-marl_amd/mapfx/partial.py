@@ -110,7 +110,9 @@ class MarlPartialBatch:
         self.node = z((E, N), torch.uint8)
         self.edge = z((E, N), torch.int32)
         self.total_coll = z((E,), torch.int32)
-        self.goal_dist = z((E, N, self.H * self.W), torch.int16)
+        gd_dt = torch.int32 if lib.mapfx_partial_goal_dist_elem_size(self.H, self.W) == 4 \
+            else torch.int16
+        self.goal_dist = z((E, N, self.H * self.W), gd_dt)
         self.out = {k: v[k] for k in ("reward", "obs", "state", "avail")}
         self._state = _abi.PState(
             pos=ptr(self.pos), goal=ptr(self.goal), init_pos=ptr(self.init_pos),

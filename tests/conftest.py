@@ -39,7 +39,7 @@ def load_fixture(name):
 
 def step_fixtures():
     return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-                  if not os.path.basename(p).startswith(("primal", "mp_", "pd_", "pw_", "runner_")))
+                  if not os.path.basename(p).startswith(("primal", "mp_", "pd_", "pw_", "runner_", "big_maps")))
 
 
 def partial_fixtures():

@@ -1,0 +1,126 @@
+"""MARL_PARTIAL_ENV at the reference's full input range (VERDICT
+r02 "what's missing" #1): N > 64 agents and maps with a side above 256, which take
+the workgroup-per-env kernel (partial_wg_kernel: agents' cells in an LDS hash, map
+in HBM) and the huge-map BFS (partial_bfs_huge_kernel).
+
+* Square cases are pinned by reference runs (tests/golden/mp_rand64_n100,
+  mp_sq300_n70, mp_orzcrop512_n3: test_gpu_partial.test_partial_matches_reference_goldens).
+* The reference's own maps with a side above 256 are all non-square, and the
+  reference itself raises IndexError on non-square maps (MARL_PARTIAL_ENV.__create_grid,
+  marl_partial.py:523-533), so those run against the CPU restatement
+  (oracle/partial_oracle.py, pinned by the goldens) on the shipped map data
+  (tests/golden/big_maps.npz, tests/golden/gen_big_maps.py): parity with the
+  reference is unpinned there beyond the shared semantics.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+KW = dict(move_reward=-0.01, stay_reward=-0.02, stay_goal_reward=0.5, node_collide_reward=-1.5,
+          edge_collide_reward=-2, env_collide_reward=-3, complete_reward=1000, complete_fac=1.5,
+          gamma=0.99)
+
+
+@pytest.fixture(scope="module")
+def mapfx_mod():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import mapfx
+    return mapfx
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _mask5(avail):
+    return (np.asarray(avail, dtype=np.uint8) << np.arange(5, dtype=np.uint8)).sum(-1)
+
+
+def _big_map(name):
+    with np.load(os.path.join(GOLDEN, "big_maps.npz")) as z:
+        key = name.replace("-", "_")
+        h, w = (int(v) for v in z[key + "_hw"])
+        bits = np.unpackbits(z[key + "_bits"], bitorder="little")[:h * w]
+    return -(bits.reshape(h, w).astype(np.int8))
+
+
+def _largest_component(g):
+    from tests_helpers_partial import largest_component
+    return largest_component(g)
+
+
+def _run(mapfx_mod, grids, N, E, T, win, K, seed, crowd=False):
+    from oracle.partial_oracle import PartialEnvState
+    rng = np.random.default_rng(seed)
+    inits, goals = [], []
+    for g in grids:
+        comp = _largest_component(g)
+        free = np.argwhere(comp == 0)
+        if crowd:   # agents packed into one corner region: collisions every step
+            free = free[np.argsort(free[:, 0] + free[:, 1], kind="stable")[:max(3 * N, 64)]]
+        pick = rng.choice(len(free), size=2 * N, replace=False)
+        inits.append(free[pick[:N]])
+        goals.append(free[pick[N:]])
+    grids, inits, goals = np.array(grids), np.array(inits), np.array(goals)
+    kw = dict(KW, obs_window=win, obs_knn_agents=K, episode_limit=T + 3)
+    b = mapfx_mod.MarlPartialBatch(inits, goals, grids=grids, **kw)
+    refs = [PartialEnvState(grids[e], inits[e], goals[e], **kw) for e in range(E)]
+    H, W = grids.shape[1:]
+    assert b.goal_dist.dtype == (torch.int32 if H * W > 32767 else torch.int16)
+    for e in range(E):
+        for a in range(N):
+            assert np.array_equal(_np(b.goal_dist[e, a]).astype(np.int64), refs[e].goal_dist[a]), (e, a)
+    out = b.reset()
+    assert np.array_equal(_np(out["obs"]), np.stack([r.obs() for r in refs]).astype(np.float32))
+    assert np.array_equal(_np(out["avail"]), np.stack([_mask5(r.avail()) for r in refs]))
+    acts = rng.integers(0, 5, size=(T, E, N))
+    ncoll = 0
+    for t in range(T):
+        out = b.step(torch.from_numpy(acts[t]).cuda())
+        rr = [r.step(acts[t, e]) for e, r in enumerate(refs)]
+        rew = np.array([x[0] for x in rr], dtype=np.float64)
+        assert np.array_equal(_np(out["reward"]).view(np.uint64), rew.view(np.uint64)), t
+        assert np.array_equal(_np(b.terminated).astype(bool), np.array([x[1] for x in rr])), t
+        assert np.array_equal(_np(b.pos), np.array([r.pos for r in refs])), t
+        assert np.array_equal(_np(b.node).astype(np.int64), np.array([r.node for r in refs])), t
+        assert np.array_equal(_np(b.edge).astype(np.int64), np.array([r.edge for r in refs])), t
+        assert np.array_equal(_np(out["obs"]), np.stack([r.obs() for r in refs]).astype(np.float32)), t
+        assert np.array_equal(_np(out["state"]), np.stack([r.state() for r in refs]).astype(np.float32)), t
+        assert np.array_equal(_np(out["avail"]), np.stack([_mask5(r.avail()) for r in refs])), t
+        ncoll += int(sum(sum(r.node) + sum(r.edge) for r in refs))
+    b.check_err()
+    return ncoll
+
+
+@pytest.mark.parametrize("name,N,T,win,K", [
+    ("warehouse-20-40-10-2-1", 20, 8, 5, 5),   # 123 x 321: non-square, width > 256
+    ("den520d", 70, 5, 7, 5),                  # 257 x 256 and N > 64
+    ("brc202d", 4, 5, 5, 3),                   # 481 x 530
+    ("orz900d", 3, 4, 5, 3),                   # 656 x 1491, the largest shipped map
+])
+def test_partial_shipped_big_maps_match_oracle(mapfx_mod, name, N, T, win, K):
+    g = _big_map(name)
+    _run(mapfx_mod, [g], N, 1, T, win, K, seed=len(name))
+
+
+@pytest.mark.parametrize("S,N,E,T,win,K", [
+    (64, 100, 3, 10, 5, 5),     # N > 64 on a 64 x 64 map
+    (40, 300, 2, 8, 3, 4),      # N = 300: three agents per thread
+    (64, 1024, 1, 2, 5, 5),     # N at the limit (1024: four agents per thread)
+    (300, 12, 2, 6, 7, 5),      # sides above 256 (huge BFS, 5 words per row)
+])
+def test_partial_wg_path_matches_oracle(mapfx_mod, S, N, E, T, win, K):
+    """Random maps; N >= 300 packs the agents into one corner (collisions every step:
+    multi-occupant cells of the hash, the edge scan)."""
+    rng = np.random.default_rng(S + N)
+    grids = [np.where(rng.random((S, S)) < 0.1, -1, 0).astype(np.int8) for _ in range(E)]
+    ncoll = _run(mapfx_mod, grids, N, E, T, win, K, seed=S * 7 + N, crowd=N >= 300)
+    if N >= 300:
+        assert ncoll > 0          # the hash's multi-occupant cells and the edge scan ran

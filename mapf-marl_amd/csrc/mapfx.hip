@@ -1226,8 +1226,13 @@ __device__ __forceinline__ void stage_occ_record(const uint32_t (&R)[(WIN * WIN 
 #ifndef MAPFX_SPLIT_NT
 #define MAPFX_SPLIT_NT 1  // nontemporal (streaming) stores from the store wave
 #endif
+#ifndef MAPFX_SPLIT_ALT
+// 1: two store waves that take the steps in turn (even / odd), each spreading its
+// step over two barrier intervals (ROLE_ALT); 0: one store wave per step
+#define MAPFX_SPLIT_ALT 1
+#endif
 #ifndef MAPFX_SPLIT_WAVES
-#define MAPFX_SPLIT_WAVES 2  // 2: step + store wave; 3: step + record wave + small-output wave (slower at C2)
+#define MAPFX_SPLIT_WAVES (MAPFX_SPLIT_ALT ? 3 : 2)  // 3 without ALT: record wave + small-output wave
 #endif
 
 // `sum(rewards)` (mapf_gridworld.py:141) over a 16-lane DPP row: a naive left fold
@@ -1299,6 +1304,113 @@ __device__ __forceinline__ int2 padded_cell_rc(const Geo& g, int cell) {
 //   small outputs: derived from the info word and the centre row; the reward
 //     fold is an in-row DPP scan (row_fold16), lane LL-1 of each env stores it.
 constexpr int ROLE_ALL = 0, ROLE_REC = 1, ROLE_SMALL = 2;
+
+// ROLE_ALT (MAPFX_SPLIT_ALT): store wave `par` takes the steps q with q % 2 == par.
+// The step wave publishes step q's image at barrier q + 2 (image (q + 1) & 1, not
+// rewritten before barrier q + 3).  Interval q + 2 .. q + 3 ("a"): read the image,
+// build the record and stage it in the wave's own LDS image, keep the info word and
+// the node flag; interval q + 3 .. q + 4 ("b"): read the staged record back, store
+// it with lane-contiguous 16-byte stores, derive and store the per-agent and per-env
+// outputs and fold the reward.  Each store wave thus carries half a step of work per
+// barrier interval, and the block has three waves whose chains overlap.
+template <int WIN, int LL, bool OCC>
+__device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a, unsigned char* sp,
+                                                     unsigned char* own, int env0, int lane, int par) {
+  typedef __attribute__((address_space(1))) unsigned char gbyte;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef int i32x2 __attribute__((ext_vector_type(2)));
+  using SL = SplitLayout<WIN, LL>;
+  constexpr int H2 = WIN / 2, REC = OCC ? WIN * WIN : SL::REC, NQ = SL::SLOT / 16;
+  constexpr int RCH = 4 * REC;                  // 16-byte chunks of the wave's 64 records
+  constexpr int NRC = (RCH + 63) / 64;
+  const int T = a.T;
+  const uint32_t E = (uint32_t)g.E, EN = E * (uint32_t)LL;
+  const int slot = lane / LL, ag = lane % LL;
+  const uint32_t env = (uint32_t)(env0 + slot), ag0 = (uint32_t)env0 * LL;
+  const u32x4* ost = (const u32x4*)__builtin_assume_aligned(own, 16);
+  uint32_t k_nc = 0, k_nb = 0, k_fl = 0, k_t = 0, k_node = 0;  // step q's info, kept from a to b
+
+  auto part_b = [&](uint32_t q) {
+    u32x4 rv[NRC];
+#pragma unroll
+    for (int k = 0; k < NRC; ++k) rv[k] = ost[(k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0];
+    gbyte* rec = (gbyte*)(OCC ? a.obs_window_occ : a.obs_window) + (q * EN + ag0) * (uint32_t)REC;
+#pragma unroll
+    for (int k = 0; k < NRC; ++k)
+      if (k < NRC - 1 || lane + 64 * k < RCH)
+        split_store((__attribute__((address_space(1))) u32x4*)(rec + 16u * (lane + 64 * k)), rv[k]);
+    const uint32_t fl = k_fl;
+    const uint32_t nzn = (((k_nb & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
+    const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
+    const uint32_t edge = fl >> 8, node = k_node;
+    double rr = 0.0;  // reward (:94-130, exact fp64 op order)
+    if (fl & SF_LIVE) {
+      if (!(fl & SF_DNOLD)) {
+        if (fl & SF_ENVC) rr = rr + g.collide_rew;
+        rr = rr + g.step_rew;
+      }
+      rr = rr + g.collide_rew * (double)node;
+      rr = rr + g.collide_rew * (double)edge;
+    }
+    const uint32_t ai = q * EN + ag0 + lane;
+    const int2 rc = padded_cell_rc(g, (int)k_nc);
+    split_store((__attribute__((address_space(1))) i32x2*)((gbyte*)a.traj_pos + 8u * ai), i32x2{rc.x, rc.y});
+    split_store((gbyte*)a.node + ai, (unsigned char)node);
+    split_store((gbyte*)a.edge + ai, (unsigned char)edge);
+    split_store((gbyte*)a.avail + ai, (unsigned char)availm);
+    split_store((gbyte*)a.traj_done + ai, (unsigned char)(fl & SF_DONE));
+    const double Rs = row_fold16(rr);  // `sum(rewards)` (:141): lane LL-1 holds the total
+    if (ag == LL - 1) {
+      const uint32_t ei = q * E + env;
+      split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), Rs);
+      split_store((__attribute__((address_space(1))) int*)((gbyte*)a.traj_t + 4u * ei), (int)k_t);
+      split_store((gbyte*)a.term + ei, (unsigned char)((fl & SF_ALLDONE) ? 1 : 0));
+      if (a.reward_f32) a.reward_f32[ei] = (float)Rs;
+      if (a.err && (fl & SF_SKIP)) atomicCAS(a.err, 0, (int)env + 1);
+    }
+  };
+
+  const int rounds = T > 0 ? T + 1 : 0;
+  for (int s = 1; s <= rounds; ++s) {
+    split_barrier();
+    if (s == 1) continue;
+    const int q = s - 2;
+    if ((q & 1) == par) {  // a(q)
+      const u32x4* sl = (const u32x4*)__builtin_assume_aligned(
+          sp + ((s - 1) & 1) * g.wv_split_buf + lane * SLOT_LANE, 16);
+      uint32_t w[4 * NQ];
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const u32x4 v = sl[SLOT_CHUNK * i];
+        w[4 * i] = v.x;
+        w[4 * i + 1] = v.y;
+        w[4 * i + 2] = v.z;
+        w[4 * i + 3] = v.w;
+      }
+      const uint32_t* qx = w + 4;
+      const int o = ((int)w[0] - H2) & 3;
+      if constexpr (OCC) {
+        uint32_t R[(WIN * WIN + 3) / 4 + 1];
+        occ_words<WIN>(qx, o, R);
+        stage_occ_record<WIN>(R, lds_addr(own + lane * REC));
+      } else {
+        uint32_t R[4 * WIN];
+        window_regs<WIN>(qx, o, R);
+        stage_record<WIN>(R, own + lane * REC);
+      }
+      // node collision (:344-362): post-step count = c - 1 + obstacle >= 2 (centre cell)
+      const uint32_t ctr = (__builtin_amdgcn_alignbyte(qx[WIN + H2], qx[H2], o) >> (8 * H2)) & 0xFFu;
+      k_node = ((ctr & 0x7Fu) + (ctr >> 7) >= 3u && !(w[2] & SF_SKIP)) ? 1u : 0u;
+      k_nc = w[0], k_nb = w[1], k_fl = w[2], k_t = w[3];
+    } else if (q >= 1) {   // b(q - 1)
+      part_b((uint32_t)(q - 1));
+    }
+  }
+  if (T > 0 && ((T - 1) & 1) == par) {  // the last step's b part
+    wave_fence();
+    part_b((uint32_t)(T - 1));
+  }
+}
 
 template <int WIN, int LL, int ROLE, bool OCC = false>
 __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, unsigned char* sp,
@@ -1447,14 +1559,17 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   MAPFX_HOT_APPLY(a, g);
   extern __shared__ __align__(16) unsigned char lds[];
   static_assert(!SPLIT || (ROLL && FULLW && RUNNER && LL == 16 && WIN > 0), "split: runner rollout, N = 16");
-  static_assert(!OCC || (SPLIT && MAPFX_SPLIT_WAVES == 2), "occupancy records: two-wave split only");
+  static_assert(!OCC || (SPLIT && (MAPFX_SPLIT_ALT || MAPFX_SPLIT_WAVES == 2)), "occupancy records: one store wave or ALT");
   if constexpr (SPLIT) {
     if (threadIdx.x >= 64) {  // the output side of the split
       if (MAPFX_PRIO_STORE) __builtin_amdgcn_s_setprio(MAPFX_PRIO_STORE);
       const int e0 = xcd_block(blockIdx.x, g.nblk) * (64 / LL);
       unsigned char* sp = lds + g.wv_off_split;
       unsigned char* own = sp + 2 * g.wv_split_buf;
-      if (MAPFX_SPLIT_WAVES == 2) split_store_wave<WIN, LL, ROLE_ALL, OCC>(g, a, sp, own, e0, threadIdx.x & 63);
+      if (MAPFX_SPLIT_ALT)
+        split_store_wave_alt<WIN, LL, OCC>(g, a, sp, own + (threadIdx.x >= 128 ? 64 * (OCC ? WIN * WIN : 2 * WIN * WIN) : 0),
+                                           e0, threadIdx.x & 63, threadIdx.x >= 128 ? 1 : 0);
+      else if (MAPFX_SPLIT_WAVES == 2) split_store_wave<WIN, LL, ROLE_ALL, OCC>(g, a, sp, own, e0, threadIdx.x & 63);
       else if (threadIdx.x < 128) split_store_wave<WIN, LL, ROLE_REC>(g, a, sp, own, e0, threadIdx.x & 63);
       else split_store_wave<WIN, LL, ROLE_SMALL>(g, a, sp, own, e0, threadIdx.x & 63);
       return;
@@ -2081,7 +2196,7 @@ int check_hip(hipError_t e, const char* what) {
 template <int WIN>
 KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split, bool occ) {
   if (occ) {  // obs_window_occ: only the store-wave split writes it on the wave path
-    if constexpr (WIN > 0 && MAPFX_SPLIT_WAVES == 2) {
+    if constexpr (WIN > 0 && (MAPFX_SPLIT_ALT || MAPFX_SPLIT_WAVES == 2)) {
       if (roll && runner && split && fullw && L == 16) return mapf_wave_kernel<WIN, true, true, true, 16, true, true>;
     }
     return nullptr;

@@ -508,6 +508,23 @@ PARTIAL_YAML = dict(  # MARL-curve-main/src/config/envs/marl_partial.yaml:3-23
     env_collide_reward=-2000, complete_reward=1000, complete_fac=1.5, gamma=0.99)
 
 
+def profile_traffic(leg, **match):
+    """(traffic bytes per unit, source) from profiles/pmc_<leg>.json when every `match`
+    key equals the profile's (the profile was taken of this exact workload), else
+    (None, None).  The file is written by tools/pmc_traffic.py from separate
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md corrections)."""
+    path = os.path.join(REPO, "profiles", "pmc_%s.json" % leg)
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if any(pm.get(k) != v for k, v in match.items()) or not pm.get("traffic_bytes_per_launch"):
+        return None, None
+    return pm["traffic_bytes_per_launch"], "%s: %s" % (os.path.relpath(path, REPO),
+                                                       pm.get("command", "rocprofv3 --pmc passes"))
+
+
 def partial_bytes_per_env_step(N, D, HW):
     """Algorithmic HBM bytes of one MARL_PARTIAL env step (state round-trips HBM):
     reads actions N + state 23N + 13 + goal/init 16N + 2 goal-distance reads 4N +
@@ -592,6 +609,8 @@ def run_partial(args, dist, rank, world, local):
     D = b.obs_dim
     bpes = partial_bytes_per_env_step(N, D, S * S)
     achieved = E * bpes / (kern_ms * 1e-3) / 1e9
+    # traffic per launch (one env step of E envs) from the PMC profile of this workload
+    traffic, traffic_src = profile_traffic("partial", E=E, N=N, S=S)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = partial_cpu_baseline(inst, S, N, args.cpu_seconds)
@@ -613,7 +632,8 @@ def run_partial(args, dist, rank, world, local):
             "eager_ms_per_step": round(eager_ms, 5),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "bytes_per_env_step": bpes},
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "bytes_per_env_step": bpes, "bytes_per_launch": E * bpes},
             "cpu_baseline": cpu}), flush=True)
     if dist:
         dist.barrier()
@@ -673,6 +693,7 @@ def run_primal(args, dist, rank, world, local):
     bpc = primal_bytes_per_call(s_obs)
     launch_bytes = E * (KC * bpc + (8 + 8 + 8) * N + inst["bits"].shape[1])  # + pos/goal in, pos out
     achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
+    traffic, traffic_src = profile_traffic("primal", E=E, N=N, K=KC, s=s_obs)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         from oracle.primal_dyn_oracle import PrimalWorld
@@ -706,7 +727,8 @@ def run_primal(args, dist, rank, world, local):
             "kernel_ms_per_launch": round(kern_ms, 5),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None, "bytes_per_call": bpc, "bytes_per_launch": int(launch_bytes)},
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "bytes_per_call": bpc, "bytes_per_launch": int(launch_bytes)},
             "cpu_baseline": cpu}), flush=True)
     if dist:
         dist.barrier()
@@ -786,6 +808,15 @@ def run_runner(args, dist, rank, world, local):
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = partial_cpu_baseline(inst, S, N, args.cpu_seconds)
+    # roofline of the runner step on the wall clock (the MAC's torch kernels and the
+    # launch gaps included): per env step, the env step's own bytes plus the
+    # EpisodeBatch rows the runner writes (episode_buffer.py:100-134 layouts: obs f32,
+    # state f32, avail_actions i32, actions i64, actions_onehot f32, reward f32,
+    # terminated u8, filled i64) and the MAC's read of the avail row
+    D = info["obs_shape"]
+    row_bytes = 4 * N * D + 4 * 3 + 4 * 5 * N + 8 * N + 4 * 5 * N + 4 + 1 + 8 + 4 * 5 * N
+    bpes = partial_bytes_per_env_step(N, D, S * S) + row_bytes
+    achieved = steps * world * bpes / elapsed / 1e9
     if rank == 0:
         print(json.dumps({
             "metric": "ParallelRunner env-steps/sec (agents x envs) into EpisodeBatch, marl_partial yaml",
@@ -799,6 +830,11 @@ def run_runner(args, dist, rank, world, local):
                                    "mapfx.episode.DeviceEpisodeBatch storage" % B,
                        "envs_total": B * world, "agents": N, "parallelism": "env-shard x%d" % world},
             "env_steps_per_s": round(steps * world / elapsed, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved / world, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / world / HBM_PEAK_GBS, 4),
+                         "traffic": None, "bytes_per_env_step": bpes, "episode_row_bytes": row_bytes,
+                         "timing": "wall clock of run() per GPU: MAC torch kernels, launch gaps "
+                                   "and the 2-step-late loop exit included"},
             "cpu_baseline": cpu}), flush=True)
     if dist:
         dist.destroy_process_group()

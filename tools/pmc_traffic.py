@@ -109,6 +109,34 @@ def lds_summary(d, kernel):
     return out
 
 
+SQ_COUNTERS = ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAIT_ANY",
+               "SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES")
+
+
+def sq_summary(d, kernel):
+    """Issue / wait counters of the kernel (one pass of 8 SQ counters), per wave and as
+    fractions of the wave cycles: where a wave's time goes (issue vs dependency wait)."""
+    out = {}
+    for c in SQ_COUNTERS:
+        v, n = pmc_values(d, kernel, c)
+        if v is not None:
+            out[c] = v
+            out["dispatches"] = n
+    w = out.get("SQ_WAVES")
+    if w:
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
+            if c in out:
+                out[c.lower()[3:] + "_per_wave"] = out[c] / w
+    wc = out.get("SQ_WAVE_CYCLES")
+    if wc:
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"):
+            if c in out:
+                out[c.lower()[3:] + "_frac_of_wave_cycles"] = out[c] / wc
+    out["note"] = ("SQ_WAIT_ANY: wave cycles waiting on any dependency (vmcnt / lgkmcnt / "
+                   "expcnt); SQ_WAIT_INST_ANY: cycles waiting for an instruction issue slot")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--trace")
@@ -122,10 +150,17 @@ def main():
     ap.add_argument("--tag", required=True, help="stats CSV name: profiles/<tag>_kernel_stats.csv")
     ap.add_argument("--lds", default=None)
     ap.add_argument("--command", default=None)
+    ap.add_argument("--sq", default=None, help="a `rocprofv3 --pmc` pass of SQ_COUNTERS")
+    ap.add_argument("--match", action="append", default=[],
+                    help="key=int stored in the summary (bench.py only uses a profile whose "
+                         "keys equal its workload's)")
     a = ap.parse_args()
     out_dir = os.path.dirname(os.path.abspath(a.out))
     os.makedirs(out_dir, exist_ok=True)
     res = {"config": a.config, "T": a.T, "E": a.E, "kernel": a.kernel}
+    for kv in a.match:
+        k, v = kv.split("=", 1)
+        res[k] = int(v)
     if a.command:
         res["command"] = a.command
     if a.trace:
@@ -146,6 +181,8 @@ def main():
         res["traffic_note"] = "(2*FETCH_SIZE + WRITE_SIZE)*1024: gfx950 FETCH_SIZE halving corrected"
     if a.lds:
         res["lds"] = lds_summary(a.lds, a.kernel)
+    if a.sq:
+        res["sq"] = sq_summary(a.sq, a.kernel)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))

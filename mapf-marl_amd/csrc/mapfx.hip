@@ -1373,7 +1373,7 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
   const int rounds = T > 0 ? T + 1 : 0;
   for (int s = 1; s <= rounds; ++s) {
     split_barrier();
-    if (s == 1) continue;
+    if (s == 1 || (MAPFX_ABLATE & 256)) continue;
     const int q = s - 2;
     if ((q & 1) == par) {  // a(q)
       const u32x4* sl = (const u32x4*)__builtin_assume_aligned(
@@ -1406,7 +1406,7 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
       part_b((uint32_t)(q - 1));
     }
   }
-  if (T > 0 && ((T - 1) & 1) == par) {  // the last step's b part
+  if (T > 0 && ((T - 1) & 1) == par && !(MAPFX_ABLATE & 256)) {  // the last step's b part
     wave_fence();
     part_b((uint32_t)(T - 1));
   }

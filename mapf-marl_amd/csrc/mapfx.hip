@@ -1281,6 +1281,9 @@ __device__ __forceinline__ void split_barrier() {
 
 template <typename P, typename V>
 __device__ __forceinline__ void split_store(P p, V v) {
+  // diagnostic ablation 512: the store waves compute everything but store nothing (a
+  // grid-size test the compiler cannot fold keeps the values live)
+  if ((MAPFX_ABLATE & 512) && blockIdx.x != 0x7FFFFFF0u) return;
   if (MAPFX_SPLIT_NT) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
@@ -1304,18 +1307,23 @@ __device__ __forceinline__ int2 padded_cell_rc(const Geo& g, int cell) {
 //   small outputs: derived from the info word and the centre row; the reward
 //     fold is an in-row DPP scan (row_fold16), lane LL-1 of each env stores it.
 constexpr int ROLE_ALL = 0, ROLE_REC = 1, ROLE_SMALL = 2;
+constexpr int SPLIT_FOLD_LDS = 256 * 8 + 32 * 64;  // ALT reward table + code ring
 
 // ROLE_ALT (MAPFX_SPLIT_ALT): store wave `par` takes the steps q with q % 2 == par.
 // The step wave publishes step q's image at barrier q + 2 (image (q + 1) & 1, not
 // rewritten before barrier q + 3).  Interval q + 2 .. q + 3 ("a"): read the image,
 // build the record and stage it in the wave's own LDS image, keep the info word and
-// the node flag; interval q + 3 .. q + 4 ("b"): read the staged record back, store
-// it with lane-contiguous 16-byte stores, derive and store the per-agent and per-env
-// outputs and fold the reward.  Each store wave thus carries half a step of work per
-// barrier interval, and the block has three waves whose chains overlap.
+// the node flag, put the agents' reward codes in the ring; interval q + 3 .. q + 4
+// ("b"): read the staged record back, store it with lane-contiguous 16-byte stores,
+// derive and store the per-agent and per-env outputs, and every 16th step fold the
+// rewards of the 16 steps.  Each store wave thus carries half a step of work per
+// barrier interval, and the block has three waves whose chains overlap.  The block's
+// throughput is VALU issue (its three waves share one SIMD's worth of issue per step),
+// so instructions are what this path saves.
 template <int WIN, int LL, bool OCC>
 __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a, unsigned char* sp,
-                                                     unsigned char* own, int env0, int lane, int par) {
+                                                     unsigned char* own, double* rtab, unsigned char* codes,
+                                                     int env0, int lane, int par) {
   typedef __attribute__((address_space(1))) unsigned char gbyte;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   typedef int i32x2 __attribute__((ext_vector_type(2)));
@@ -1330,6 +1338,42 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
   const u32x4* ost = (const u32x4*)__builtin_assume_aligned(own, 16);
   uint32_t k_nc = 0, k_nb = 0, k_fl = 0, k_t = 0, k_node = 0;  // step q's info, kept from a to b
 
+  // Rewards: an agent's reward (:94-130) is a function of five small fields, so the
+  // a part stores one CODE byte per agent (bit 0 node, bits 1-3 the SF_LIVE / SF_DNOLD
+  // / SF_ENVC flags, bits 4-7 edge; N == 16 bounds edge by 15) in a 32-step ring, and
+  // `sum(rewards)` (:141) of 16 steps x 4 envs is folded at once, one (env, step) per
+  // lane, from a table of the 256 code rewards: 16 fp64 adds per 16 steps instead of a
+  // 15-add DPP row scan per step.
+  for (int c = lane + 64 * par; c < 256; c += 128) {  // the table (both waves, before barrier 1)
+    double rr = 0.0;  // exact fp64 op order of the reference
+    if (c & SF_LIVE) {
+      if (!(c & SF_DNOLD)) {
+        if (c & SF_ENVC) rr = rr + g.collide_rew;
+        rr = rr + g.step_rew;
+      }
+      rr = rr + g.collide_rew * (double)(c & 1);
+      rr = rr + g.collide_rew * (double)(c >> 4);
+    }
+    rtab[c] = rr;
+  }
+  // steps q0 .. q0 + cnt - 1 (one 16-step batch of the ring): lane = (env e, step j)
+  auto fold_batch = [&](uint32_t q0, int cnt) {
+    const int j = lane & 15, e = lane >> 4;
+    if (j < cnt) {
+      const u32x4 cv = *(const u32x4*)__builtin_assume_aligned(codes + ((q0 + j) & 31) * 64 + e * 16, 16);
+      const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w};
+      double v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = rtab[(cw[i >> 2] >> (8 * (i & 3))) & 0xFFu];
+      double R = 0.0;  // the naive left fold in agent order
+#pragma unroll
+      for (int i = 0; i < 16; ++i) R = R + v[i];
+      const uint32_t ei = (q0 + j) * E + (uint32_t)env0 + e;
+      split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), R);
+      if (a.reward_f32) a.reward_f32[ei] = (float)R;
+    }
+  };
+
   auto part_b = [&](uint32_t q) {
     u32x4 rv[NRC];
 #pragma unroll
@@ -1343,15 +1387,6 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
     const uint32_t nzn = (((k_nb & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
     const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
     const uint32_t edge = fl >> 8, node = k_node;
-    double rr = 0.0;  // reward (:94-130, exact fp64 op order)
-    if (fl & SF_LIVE) {
-      if (!(fl & SF_DNOLD)) {
-        if (fl & SF_ENVC) rr = rr + g.collide_rew;
-        rr = rr + g.step_rew;
-      }
-      rr = rr + g.collide_rew * (double)node;
-      rr = rr + g.collide_rew * (double)edge;
-    }
     const uint32_t ai = q * EN + ag0 + lane;
     const int2 rc = padded_cell_rc(g, (int)k_nc);
     split_store((__attribute__((address_space(1))) i32x2*)((gbyte*)a.traj_pos + 8u * ai), i32x2{rc.x, rc.y});
@@ -1359,19 +1394,26 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
     split_store((gbyte*)a.edge + ai, (unsigned char)edge);
     split_store((gbyte*)a.avail + ai, (unsigned char)availm);
     split_store((gbyte*)a.traj_done + ai, (unsigned char)(fl & SF_DONE));
-    const double Rs = row_fold16(rr);  // `sum(rewards)` (:141): lane LL-1 holds the total
     if (ag == LL - 1) {
       const uint32_t ei = q * E + env;
-      split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), Rs);
       split_store((__attribute__((address_space(1))) int*)((gbyte*)a.traj_t + 4u * ei), (int)k_t);
       split_store((gbyte*)a.term + ei, (unsigned char)((fl & SF_ALLDONE) ? 1 : 0));
-      if (a.reward_f32) a.reward_f32[ei] = (float)Rs;
       if (a.err && (fl & SF_SKIP)) atomicCAS(a.err, 0, (int)env + 1);
     }
+    // the batch ends here: every code of it is in the ring (this wave's a(q) one
+    // interval ago, the other wave's a(q - 1) before the last barrier)
+    if ((q & 15u) == 15u || q + 1 == (uint32_t)T) fold_batch(q & ~15u, (int)(q & 15u) + 1);
   };
 
   const int rounds = T > 0 ? T + 1 : 0;
   for (int s = 1; s <= rounds; ++s) {
+#ifdef MAPFX_STAMPS  // diagnostic: end of round s - 1's work (columns 5 / 7 of row s - 1)
+    if (s > 1) {
+      unsigned long long t_;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+      if (blockIdx.x == 0 && lane == 0 && s - 1 < 256) g_stamps[(s - 1) * 8 + 5 + 2 * par] = t_;
+    }
+#endif
     split_barrier();
     if (s == 1 || (MAPFX_ABLATE & 256)) continue;
     const int q = s - 2;
@@ -1402,6 +1444,8 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
       const uint32_t ctr = (__builtin_amdgcn_alignbyte(qx[WIN + H2], qx[H2], o) >> (8 * H2)) & 0xFFu;
       k_node = ((ctr & 0x7Fu) + (ctr >> 7) >= 3u && !(w[2] & SF_SKIP)) ? 1u : 0u;
       k_nc = w[0], k_nb = w[1], k_fl = w[2], k_t = w[3];
+      codes[(q & 31) * 64 + lane] =
+          (unsigned char)(k_node | (k_fl & (SF_LIVE | SF_DNOLD | SF_ENVC)) | ((k_fl >> 4) & 0xF0u));
     } else if (q >= 1) {   // b(q - 1)
       part_b((uint32_t)(q - 1));
     }
@@ -1566,9 +1610,12 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
       const int e0 = xcd_block(blockIdx.x, g.nblk) * (64 / LL);
       unsigned char* sp = lds + g.wv_off_split;
       unsigned char* own = sp + 2 * g.wv_split_buf;
+      constexpr int RECB = OCC ? WIN * WIN : 2 * WIN * WIN;  // one wave's staged image: 64 * RECB
+      double* rtab = (double*)(own + 2 * 64 * RECB);          // ALT: reward table + code ring
       if (MAPFX_SPLIT_ALT)
-        split_store_wave_alt<WIN, LL, OCC>(g, a, sp, own + (threadIdx.x >= 128 ? 64 * (OCC ? WIN * WIN : 2 * WIN * WIN) : 0),
-                                           e0, threadIdx.x & 63, threadIdx.x >= 128 ? 1 : 0);
+        split_store_wave_alt<WIN, LL, OCC>(g, a, sp, own + (threadIdx.x >= 128 ? 64 * RECB : 0), rtab,
+                                           (unsigned char*)(rtab + 256), e0, threadIdx.x & 63,
+                                           threadIdx.x >= 128 ? 1 : 0);
       else if (MAPFX_SPLIT_WAVES == 2) split_store_wave<WIN, LL, ROLE_ALL, OCC>(g, a, sp, own, e0, threadIdx.x & 63);
       else if (threadIdx.x < 128) split_store_wave<WIN, LL, ROLE_REC>(g, a, sp, own, e0, threadIdx.x & 63);
       else split_store_wave<WIN, LL, ROLE_SMALL>(g, a, sp, own, e0, threadIdx.x & 63);
@@ -1648,15 +1695,19 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   int nxt[AB];
   const bool act_mem = do_step && !a.use_rng;
   const auto fetch = [&](int s0) {
+    // s0 is opaque here: the row offsets are formed at the fetch (scalar row offset +
+    // the lane's offset) instead of AB address registers stepped every loop iteration
+    int sb = s0;
+    asm volatile("" : "+s"(sb));
     if (!ROLL || a.act_dtype != MAPFX_I8) {
 #pragma unroll
       for (int k = 0; k < AB; ++k)
-        nxt[k] = (has && s0 + k < T) ? load_action(a.actions, a.act_dtype, (uint32_t)(s0 + k) * EN + oa) : 4;
+        nxt[k] = (has && sb + k < T) ? load_action(a.actions, a.act_dtype, (uint32_t)(sb + k) * EN + oa) : 4;
     } else {  // int8 buffer: AB unconditional loads (clamped addresses)
       const int8_t* ap = (const int8_t*)a.actions;
       const uint32_t oc_ = has ? oa : 0u;
 #pragma unroll
-      for (int k = 0; k < AB; ++k) nxt[k] = ap[(uint32_t)min(s0 + k, T - 1) * EN + oc_];
+      for (int k = 0; k < AB; ++k) nxt[k] = (ap + (uint32_t)min(sb + k, T - 1) * EN)[oc_];
     }
   };
   if (act_mem) fetch(0);
@@ -2244,7 +2295,9 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
                            (uintptr_t)a.node | (uintptr_t)a.edge | (uintptr_t)a.avail |
                            (uintptr_t)a.traj_done | (uintptr_t)a.reward | (uintptr_t)a.traj_t;
     // + staged-record images of the store wave (2 x 64 records)
-    const int split_lds = g.wv_lds + 2 * g.wv_split_buf + 2 * 64 * (occ ? g.wlen / 2 : g.wlen);
+    // (+ ALT: the 256-entry reward table and the 32-step code ring)
+    const int split_lds = g.wv_lds + 2 * g.wv_split_buf + 2 * 64 * (occ ? g.wlen / 2 : g.wlen) +
+                          (MAPFX_SPLIT_ALT ? SPLIT_FOLD_LDS : 0);
     const bool split = MAPFX_SPLIT && runner && fullw && g.L == 16 && g.wv_split_buf > 0 &&
                        split_lds <= 64 * 1024 && (al16 & 15) == 0;
     KernelFn fn = pick_wave_kernel((a.obs_window || occ) ? g.window : 0, roll, fullw, runner, g.L, split, occ);

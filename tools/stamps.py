@@ -46,6 +46,20 @@ def main():
     print("  %-18s %7.0f %7.0f" % ("loop+actions", np.median(nxt), nxt.mean()))
     tot = st[2:, 0] - st[1:-1, 0]
     print("  %-18s %7.0f %7.0f" % ("step total", np.median(tot), tot.mean()))
+    if st[2:T - 1, 5].any():  # store-wave split: busy time of each wave per barrier interval
+        rel = st[1:T - 2, 6]          # release of barrier s (the step wave's stamp 6 of s - 1)
+        rows = slice(2, T - 1)
+        iv = st[rows, 6] - rel
+        print("  split path, cycles per barrier interval (median / mean), from the release:")
+        for name, col in (("step wave busy", 4), ("store wave 0 busy", 5), ("store wave 1 busy", 7)):
+            d = st[rows, col] - rel
+            print("  %-18s %7.0f %7.0f" % (name, np.median(d), d.mean()))
+        print("  %-18s %7.0f %7.0f" % ("interval", np.median(iv), iv.mean()))
+        for par, col in ((0, 5), (1, 7)):
+            d = st[rows, col] - rel
+            q = np.arange(2, T - 1) - 2
+            a_, b_ = d[(q & 1) == par], d[(q & 1) != par]
+            print("  store wave %d: a parts %6.0f, b parts %6.0f (median)" % (par, np.median(a_), np.median(b_)))
 
 
 if __name__ == "__main__":

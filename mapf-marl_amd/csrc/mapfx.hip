@@ -1586,15 +1586,17 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
 //   D  step s's neighbour bytes, dones, t and all-done ballot  (dependency chain)
 // so only A and D (a few dozen instructions) sit on the serial chain between
 // steps.  The last step's heavy part and tails run after the loop.
-// Wave priorities of the split (s_setprio): the store wave's per-step chain is the
-// longer one (the step wave waits for it at the hand-over barrier), so it wins issue
-// arbitration against the other blocks' waves on its SIMD.  C2: -3 % (T = 20) to
-// -6 % (T = 64) kernel time; raising the step wave instead measured neutral.
+// Wave priorities of the split (s_setprio): with the ALT store waves and the batched
+// reward fold the STEP wave's chain is the longer one (block-0 stamps at C2: step wave
+// busy ~2300 cycles per barrier interval, each store wave ~850), so the step wave wins
+// issue arbitration against the other blocks' store waves on its SIMD: C2 T = 20
+// 25.0 -> 23.5 us (round 3; with the round-2 single store wave the store side was the
+// long chain and its priority paid instead).
 #ifndef MAPFX_PRIO_STEP
-#define MAPFX_PRIO_STEP 0
+#define MAPFX_PRIO_STEP 3
 #endif
 #ifndef MAPFX_PRIO_STORE
-#define MAPFX_PRIO_STORE 3
+#define MAPFX_PRIO_STORE 0
 #endif
 template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false, bool OCC = false>
 __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g0) {
@@ -1608,6 +1610,18 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
     if (threadIdx.x >= 64) {  // the output side of the split
       if (MAPFX_PRIO_STORE) __builtin_amdgcn_s_setprio(MAPFX_PRIO_STORE);
       const int e0 = xcd_block(blockIdx.x, g.nblk) * (64 / LL);
+      if (g.wv_fast) {  // the store waves build their share of the padded maps (rows
+        // ag + 16 w of each env, w = this wave's index: the step wave takes w = 0), then
+        // the barrier the step wave meets after its own rows
+        const int l64 = threadIdx.x & 63, sl = l64 / LL;
+        const uint32_t* src = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)(e0 + sl) * g.map_stride));
+        uint32_t pf[1][3];
+        const int bl = l64 % LL + LL * (threadIdx.x >> 6);
+        fast_row_prefetch<1>(g, src, bl, LL * MAPFX_SPLIT_WAVES, pf);
+        build_map_rows_fast<MAPFX_FAST_WPR, 1>(g, (uint32_t*)(lds + g.wv_off_map + sl * g.map_env_bytes), src,
+                                               bl, LL * MAPFX_SPLIT_WAVES, pf);
+      }
+      split_barrier();
       unsigned char* sp = lds + g.wv_off_split;
       unsigned char* own = sp + 2 * g.wv_split_buf;
       constexpr int RECB = OCC ? WIN * WIN : 2 * WIN * WIN;  // one wave's staged image: 64 * RECB
@@ -1666,9 +1680,11 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   const uint32_t EN = (uint32_t)(g.E * N);
   // bitmap words of this lane's first map rows (fast build): issued first
   const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared || !env_ok ? 0 : (long long)env * g.map_stride));
-  constexpr int RPF = 4;
+  // (the split kernel's three waves build the rows together: lane ag + 16 w of 48)
+  constexpr int RPF = SPLIT ? 1 : 4;
+  const int bl = ag, bnl = SPLIT ? LL * MAPFX_SPLIT_WAVES : L;
   uint32_t pfw[RPF][3];
-  if (g.wv_fast) fast_row_prefetch<RPF>(g, bsrc, ag, L, pfw);
+  if (g.wv_fast) fast_row_prefetch<RPF>(g, bsrc, bl, bnl, pfw);
   int tcur = env_ok ? a.t[env] : 0;  // (issued first: its pointer is preloaded)
   int cur = 0, gcell = -1, st = 0;  // padded cell of the agent / of its goal
   bool dn = false;
@@ -1716,14 +1732,15 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   if (env_ok && !g.wv_fast) {
     for (int w = ag; w < g.bits_words; w += L) bitsL[w] = bsrc[w];
   }
-  if (ROLL) {  // both reward rows start at +0.0 (folds of steps < 0 read them)
+  if (ROLL && !SPLIT) {  // both reward rows start at +0.0 (folds of steps < 0 read them)
     for (int i = lane64; i < 2 * rew_buf; i += 64) rewL[i] = 0.0;
   }
   if (!g.wv_fast) wave_fence();
   PSTAMP(1);
-  if (g.wv_fast) build_map_rows_fast<MAPFX_FAST_WPR, RPF>(g, map32, bsrc, ag, L, pfw);
+  if (g.wv_fast) build_map_rows_fast<MAPFX_FAST_WPR, RPF>(g, map32, bsrc, bl, bnl, pfw);
   else build_map_rows_c(g, map32, bitsL, ag, L);
-  wave_fence();
+  if constexpr (SPLIT) split_barrier();  // + the store waves' rows
+  else wave_fence();
   PSTAMP(2);
   if (has) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
   wave_fence();

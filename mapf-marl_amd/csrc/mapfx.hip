@@ -1224,16 +1224,32 @@ __device__ __forceinline__ void stage_occ_record(const uint32_t (&R)[(WIN * WIN 
 #define MAPFX_SPLIT 1  // store-wave split for the N = 16 runner rollout
 #endif
 #ifndef MAPFX_SPLIT_NT
-#define MAPFX_SPLIT_NT 1  // nontemporal (streaming) stores from the store wave
+// 1: nontemporal stores from the store waves.  Round 3 (C2, rollout T sweep):
+// plain stores take T = 64 from 71 to 55-57 us and leave T = 20 unchanged.
+#define MAPFX_SPLIT_NT 0
 #endif
 #ifndef MAPFX_SPLIT_ALT
 // 1: two store waves that take the steps in turn (even / odd), each spreading its
 // step over two barrier intervals (ROLE_ALT); 0: one store wave per step
 #define MAPFX_SPLIT_ALT 1
 #endif
-#ifndef MAPFX_SPLIT_WAVES
-#define MAPFX_SPLIT_WAVES (MAPFX_SPLIT_ALT ? 3 : 2)  // 3 without ALT: record wave + small-output wave
+#ifndef MAPFX_SPLIT_MOVE
+// 1 (with ALT): the step side is two waves -- a MOVE wave that runs the dynamics from
+// the static obstacle flags and a MAP wave that keeps the agent-count map and builds
+// the step images -- whenever no agent stands, or is reset, on an obstacle (then a
+// move is refused exactly on obstacle / border cells, mapf_gridworld.py:319-342);
+// otherwise the block runs the one-wave step side (wave 1 idles).  Measured round 3
+// at C2: the step side alone 0.65 -> 0.57 us/step, but the kernel is bound by its
+// store side (T = 20: 23.2 vs 23.0 us, T = 64: 57.4 vs 55.4 us with plain stores),
+// so the three-wave split stays the default.
+#define MAPFX_SPLIT_MOVE 0
 #endif
+#ifndef MAPFX_SPLIT_WAVES
+#define MAPFX_SPLIT_WAVES (MAPFX_SPLIT_MOVE ? 4 : MAPFX_SPLIT_ALT ? 3 : 2)  // 3 without ALT: record wave + small-output wave
+#endif
+// step-side waves ahead of the store waves
+#define MAPFX_SPLIT_SW0 (MAPFX_SPLIT_MOVE ? 2 : 1)
+constexpr int SPLIT_RING_LDS = 2 * 64 * 16;  // MOVE -> MAP ring: 2 steps x 64 lanes x u32x4
 
 // `sum(rewards)` (mapf_gridworld.py:141) over a 16-lane DPP row: a naive left fold
 // ((0 + r_0) + r_1) + ... in agent order.  Iteration k makes lane k's running sum
@@ -1276,6 +1292,7 @@ constexpr uint32_t SF_DONE = 1, SF_LIVE = 2, SF_DNOLD = 4, SF_ENVC = 8, SF_SKIP 
 // Workgroup barrier that waits for this wave's LDS traffic only: outstanding
 // global stores stay in flight (a __syncthreads() would drain them every step).
 __device__ __forceinline__ void split_barrier() {
+  if (MAPFX_ABLATE & 1024) return;  // diagnostic only: no hand-over (results are garbage)
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
@@ -1377,11 +1394,13 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
   auto part_b = [&](uint32_t q) {
     u32x4 rv[NRC];
 #pragma unroll
-    for (int k = 0; k < NRC; ++k) rv[k] = ost[(k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0];
+    for (int k = 0; k < NRC; ++k)
+      rv[k] = (MAPFX_ABLATE & 32768) ? u32x4{q, (uint32_t)lane, (uint32_t)k, 0u}  // diagnostic: no LDS read
+                                     : ost[(k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0];
     gbyte* rec = (gbyte*)(OCC ? a.obs_window_occ : a.obs_window) + (q * EN + ag0) * (uint32_t)REC;
 #pragma unroll
     for (int k = 0; k < NRC; ++k)
-      if (k < NRC - 1 || lane + 64 * k < RCH)
+      if ((k < NRC - 1 || lane + 64 * k < RCH) && (!(MAPFX_ABLATE & 16384) || blockIdx.x == 0x7FFFFFF0u))
         split_store((__attribute__((address_space(1))) u32x4*)(rec + 16u * (lane + 64 * k)), rv[k]);
     const uint32_t fl = k_fl;
     const uint32_t nzn = (((k_nb & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
@@ -1435,6 +1454,25 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
         uint32_t R[(WIN * WIN + 3) / 4 + 1];
         occ_words<WIN>(qx, o, R);
         stage_occ_record<WIN>(R, lds_addr(own + lane * REC));
+      } else if (MAPFX_ABLATE & 4096) {  // diagnostic: the staging writes of raw words (no VALU)
+        typedef __attribute__((address_space(3))) uint32_t lds_u32;
+        typedef __attribute__((address_space(3))) uint16_t lds_u16;
+        const uint32_t ra = lds_addr(own + lane * REC);
+        lds_u32* d = (lds_u32*)(uintptr_t)(ra + (ra & 2));
+#pragma unroll
+        for (int j = 0; j < (REC - 2) / 4; ++j) d[j] = qx[j % (2 * WIN)];
+        *(lds_u16*)(uintptr_t)(ra + ((ra & 2) ? 0 : REC - 2)) = (uint16_t)qx[0];
+      } else if (MAPFX_ABLATE & 8192) {  // diagnostic: the record's VALU, one LDS write
+        typedef __attribute__((address_space(3))) uint16_t lds_u16;
+        uint32_t R[4 * WIN];
+        window_regs<WIN>(qx, o, R);
+        constexpr int NW = (REC + 3) / 4;
+        uint32_t wv[NW];
+        rec_words<WIN>(R, wv, std::make_integer_sequence<int, NW>{});
+        uint32_t x = 0;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) x ^= __builtin_amdgcn_alignbyte(wv[(j + 1) % NW], wv[j], (lane & 1) * 2);
+        *(lds_u16*)(uintptr_t)lds_addr(own + lane * REC) = (uint16_t)x;
       } else {
         uint32_t R[4 * WIN];
         window_regs<WIN>(qx, o, R);
@@ -1599,7 +1637,10 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
 #define MAPFX_PRIO_STORE 0
 #endif
 template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false, bool OCC = false>
-__global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g0) {
+// (split: 4 blocks per CU must be resident -- one wave per SIMD of each role -- so the
+// register budget is that of MAPFX_SPLIT_WAVES waves per SIMD)
+__global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? MAPFX_SPLIT_WAVES : 1)
+    mapf_wave_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g0) {
   Args a = a0;
   Geo g = g0;
   MAPFX_HOT_APPLY(a, g);
@@ -1607,7 +1648,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   static_assert(!SPLIT || (ROLL && FULLW && RUNNER && LL == 16 && WIN > 0), "split: runner rollout, N = 16");
   static_assert(!OCC || (SPLIT && (MAPFX_SPLIT_ALT || MAPFX_SPLIT_WAVES == 2)), "occupancy records: one store wave or ALT");
   if constexpr (SPLIT) {
-    if (threadIdx.x >= 64) {  // the output side of the split
+    if (threadIdx.x >= 64 * MAPFX_SPLIT_SW0) {  // the output side of the split
       if (MAPFX_PRIO_STORE) __builtin_amdgcn_s_setprio(MAPFX_PRIO_STORE);
       const int e0 = xcd_block(blockIdx.x, g.nblk) * (64 / LL);
       if (g.wv_fast) {  // the store waves build their share of the padded maps (rows
@@ -1626,10 +1667,10 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
       unsigned char* own = sp + 2 * g.wv_split_buf;
       constexpr int RECB = OCC ? WIN * WIN : 2 * WIN * WIN;  // one wave's staged image: 64 * RECB
       double* rtab = (double*)(own + 2 * 64 * RECB);          // ALT: reward table + code ring
+      const int par = (int)(threadIdx.x >> 6) - MAPFX_SPLIT_SW0;  // ALT: this wave's step parity
       if (MAPFX_SPLIT_ALT)
-        split_store_wave_alt<WIN, LL, OCC>(g, a, sp, own + (threadIdx.x >= 128 ? 64 * RECB : 0), rtab,
-                                           (unsigned char*)(rtab + 256), e0, threadIdx.x & 63,
-                                           threadIdx.x >= 128 ? 1 : 0);
+        split_store_wave_alt<WIN, LL, OCC>(g, a, sp, own + par * 64 * RECB, rtab,
+                                           (unsigned char*)(rtab + 256), e0, threadIdx.x & 63, par);
       else if (MAPFX_SPLIT_WAVES == 2) split_store_wave<WIN, LL, ROLE_ALL, OCC>(g, a, sp, own, e0, threadIdx.x & 63);
       else if (threadIdx.x < 128) split_store_wave<WIN, LL, ROLE_REC>(g, a, sp, own, e0, threadIdx.x & 63);
       else split_store_wave<WIN, LL, ROLE_SMALL>(g, a, sp, own, e0, threadIdx.x & 63);
@@ -1637,6 +1678,8 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
     }
     if (MAPFX_PRIO_STEP) __builtin_amdgcn_s_setprio(MAPFX_PRIO_STEP);
   }
+  // MAPFX_SPLIT_MOVE: wave 1 is the MAP wave (it runs the prologue below with wave 0)
+  const bool is_map = SPLIT && MAPFX_SPLIT_MOVE && threadIdx.x >= 64;
   constexpr int WW = WIN * WIN;
   constexpr int H2 = WIN / 2;
   constexpr int REC = 2 * WW;  // record bytes per agent
@@ -1682,7 +1725,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared || !env_ok ? 0 : (long long)env * g.map_stride));
   // (the split kernel's three waves build the rows together: lane ag + 16 w of 48)
   constexpr int RPF = SPLIT ? 1 : 4;
-  const int bl = ag, bnl = SPLIT ? LL * MAPFX_SPLIT_WAVES : L;
+  const int bl = SPLIT ? ag + LL * (int)(threadIdx.x >> 6) : ag, bnl = SPLIT ? LL * MAPFX_SPLIT_WAVES : L;
   uint32_t pfw[RPF][3];
   if (g.wv_fast) fast_row_prefetch<RPF>(g, bsrc, bl, bnl, pfw);
   int tcur = env_ok ? a.t[env] : 0;  // (issued first: its pointer is preloaded)
@@ -1742,7 +1785,18 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   if constexpr (SPLIT) split_barrier();  // + the store waves' rows
   else wave_fence();
   PSTAMP(2);
-  if (has) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
+  // MAPFX_SPLIT_MOVE fast mode: no agent of the block stands on an obstacle, nor is
+  // reset onto one (both waves find the same answer from the same agents)
+  bool fast = false;
+  if constexpr (SPLIT && MAPFX_SPLIT_MOVE) {
+    int icell = cur;
+    if (a.autoreset && a.init_pos) {
+      const int2 p = ((const int2*)a.init_pos)[oa];
+      icell = cell0 + p.x * pitch + p.y;
+    }
+    fast = __ballot(((map[cur] | map[icell]) & 0x80u) != 0) == 0;
+  }
+  if (has && !is_map) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
   wave_fence();
 
   const auto cell_rc = [&](int cell) {  // padded cell -> (row, col); cell < 2^16, pitch < 256
@@ -1863,7 +1917,8 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
       for (int i = 4 + SL::NXW; i < SL::SLOT / 4; ++i) w[i] = 0;
 #pragma unroll
       for (int i = 0; i < SL::SLOT / 16; ++i)  // chunk-major: lanes write consecutive 16-B chunks
-        sl[SLOT_CHUNK * i] = u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+        if (!(MAPFX_ABLATE & 2048) || i == 0)   // (diagnostic 2048: the info chunk only)
+          sl[SLOT_CHUNK * i] = u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
       return;
     }
     const uint32_t so = ROLL ? (uint32_t)qs * EN : 0u;
@@ -1954,7 +2009,8 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
   const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
   const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  for (int s = 0; s < T; ++s) {
+  // the action of step s: blocks of AB steps unpacked from the prefetch, 4 per u32
+  const auto next_action = [&](int s) {
     if ((s & (AB - 1)) == 0) {  // actions of steps s .. s+AB-1, packed 4 per u32
       int v[AB];
       if (!do_step) {  // observation pass: there is no action buffer
@@ -1978,11 +2034,132 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64) mapf_wave
         actpk[k >> 2] |= u << (8 * (k & 3));
       }
     }
-    const int act = (int)(actpk[0] & 0xFFu);
+    const int act_ = (int)(actpk[0] & 0xFFu);
 #pragma unroll
     for (int k = 0; k < (AB + 3) / 4; ++k)  // shift the packed actions down one byte
       actpk[k] = (k + 1 < (AB + 3) / 4) ? __builtin_amdgcn_alignbit(actpk[k + 1], actpk[k], 8)
                                         : (actpk[k] >> 8);
+    return act_;
+  };
+
+  if constexpr (SPLIT && MAPFX_SPLIT_MOVE && WIN > 0) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int RECB = OCC ? WIN * WIN : 2 * WIN * WIN;
+    u32x4* ring = (u32x4*)__builtin_assume_aligned(
+        lds + g.wv_off_split + 2 * g.wv_split_buf + 2 * 64 * RECB + SPLIT_FOLD_LDS, 16);
+    if (is_map) {
+      if (!fast) {  // the one-wave step side runs on wave 0: only its barriers
+        for (int s = 1; s <= T + 1; ++s) split_barrier();
+        return;
+      }
+      // ---- MAP wave: step q of the MOVE wave's ring -> agent-count map, dep map,
+      // edge test (:364-383), window rows, the step image for the store waves ----
+      int mcur = cur;  // where this lane's agent stands in the count map
+      for (int s = 1; s <= T + 1; ++s) {
+        split_barrier();  // step s - 1's ring record is published
+        if (s > T) break;
+        const int q = s - 1;
+        const u32x4 r = ring[(q & 1) * 64 + lane64];
+        const int oc = (int)(r.x & 0xFFFFu), nc = (int)(r.x >> 16);
+        const uint32_t f = r.y;
+        if (__ballot(oc != mcur)) {  // the env was reset after step q - 1 (autoreset)
+          if (oc != mcur) {
+            atomicSub(&map32[mcur >> 2], 1u << ((mcur & 3) * 8));
+            atomicAdd(&map32[oc >> 2], 1u << ((oc & 3) * 8));
+          }
+        }
+        const uint32_t v = map[nc];  // the target's pre-step byte (moved lanes)
+        const bool mvd = (f & 128u) != 0;
+        const int act = (int)((f >> 8) & 0xFFu);
+        dep[oc] = (unsigned char)(mvd ? (uint32_t)act : 0x7Fu);
+        atomicAdd(&map32[oc >> 2], mvd ? 0u - (1u << ((oc & 3) * 8)) : 0u);
+        atomicAdd(&map32[nc >> 2], mvd ? 1u << ((nc & 3) * 8) : 0u);
+        uint32_t x[3 * NX];
+        {
+          const int w0 = (nc - H2 * pitch - H2) >> 2;
+          const int wpr = pitch >> 2;
+#pragma unroll
+          for (int y = 0; y < WIN; ++y) {
+            x[y] = map32[w0 + y * wpr];
+            x[WIN + y] = map32[w0 + y * wpr + 1];
+            x[2 * WIN + y] = WIN > 5 ? map32[w0 + y * wpr + 2] : 0u;
+          }
+        }
+        const uint32_t dj = dep[nc];
+        const int o8 = ((nc - H2) & 3) * 8;
+        const auto row64 = [&](int y) { return ((uint64_t)x[WIN + y] << 32) | x[y]; };
+        const uint32_t up = (uint32_t)(row64(H2 - 1) >> (o8 + 8 * H2)) & 0xFFu;
+        const uint32_t dw = (uint32_t)(row64(H2 + 1) >> (o8 + 8 * H2)) & 0xFFu;
+        const uint32_t cr = (uint32_t)(row64(H2) >> (o8 + 8 * (H2 - 1)));
+#pragma unroll
+        for (int i = 0; i < 3 * NX; ++i) qx[i] = x[i];
+        q_oc = oc;
+        q_nc = nc;
+        q_act = act;
+        q_pre = (int)(v & 0x7Fu) - 1 + (int)(v >> 7);
+        q_dj = dj;
+        q_nb = up | (dw << 8) | ((cr & 0xFFu) << 16) | (((cr >> 16) & 0xFFu) << 24);
+        q_moved = mvd;
+        q_envc = (f & SF_ENVC) != 0;
+        q_dnold = (f & SF_DNOLD) != 0;
+        q_dn = (f & SF_DONE) != 0;
+        q_live = (f & SF_LIVE) != 0;
+        q_skip = (f & SF_SKIP) != 0;
+        q_alldone = (f & SF_ALLDONE) != 0;
+        q_tcur = (int)r.z;
+        heavy(q);  // image (q + 1) & 1, published by the next barrier
+        mcur = nc;
+      }
+      return;
+    }
+    if (fast) {
+      // ---- MOVE wave: the dynamics (:85-141) from the static obstacle flags (bit 7
+      // of the count map, never touched by the MAP wave's count updates) ----
+      for (int s = 0; s < T; ++s) {
+        const int act = next_action(s);
+        const int oc = cur;
+        const bool mv = !dn && (uint32_t)act < 4u;
+        const bool obst = mv && ((nb >> ((act & 3) * 8)) & 0x80u) != 0;  // obstacle / border
+        const bool envc = obst;
+        const bool skip = (__ballot(act == 0xFF) & envmask) != 0;
+        const bool moved = mv && !obst && !skip;
+        int dlt = (act & 2) ? 1 : pitch;  // 0: up, 1: down, 2: left, 3: right
+        dlt = (act & 1) ? dlt : -dlt;
+        const int nc = moved ? oc + dlt : oc;
+        const bool dn_old = dn;
+        const bool live = !skip;
+        if (live && nc == gcell) dn = true;          // :112-114
+        if (live && tcur + 1 >= g.limit) dn = true;  // :116-117
+        if (live && !dn_old) ++st;
+        if (!skip) ++tcur;
+        const bool alldone = (__ballot(!dn) & envmask) == 0;
+        const uint32_t f = (dn ? SF_DONE : 0u) | (live ? SF_LIVE : 0u) | (dn_old ? SF_DNOLD : 0u) |
+                           (envc ? SF_ENVC : 0u) | (skip ? SF_SKIP : 0u) | (alldone ? SF_ALLDONE : 0u) |
+                           (moved ? 128u : 0u) | ((uint32_t)act << 8);
+        ring[(s & 1) * 64 + lane64] = u32x4{(uint32_t)oc | ((uint32_t)nc << 16), f, (uint32_t)tcur, 0u};
+        cur = nc;
+        if (a.autoreset && alldone) {  // the MAP wave moves the counts when it sees oc != its cell
+          const int2 p = ((const int2*)a.init_pos)[oa];
+          cur = cell0 + p.x * pitch + p.y;
+          dn = false;
+          st = 0;
+          tcur = 0;
+        }
+        nb = (uint32_t)map[cur - pitch] | ((uint32_t)map[cur + pitch] << 8) |
+             ((uint32_t)map[cur - 1] << 16) | ((uint32_t)map[cur + 1] << 24);
+        split_barrier();  // ring slot s & 1 -> MAP wave
+      }
+      split_barrier();  // the MAP wave's last image
+      ((int2*)a.pos)[oa] = cell_rc(cur);
+      a.done[oa] = dn ? 1 : 0;
+      if (a.steps) a.steps[oa] = st;
+      if (ag == 0) a.t[env] = tcur;
+      return;
+    }
+  }
+
+  for (int s = 0; s < T; ++s) {
+    const int act = next_action(s);
     STAMP(0);
     // ---------------- A: move decision on the PRE-step map (:319-342) ----------------
     const int oc = cur;
@@ -2314,7 +2491,7 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
     // + staged-record images of the store wave (2 x 64 records)
     // (+ ALT: the 256-entry reward table and the 32-step code ring)
     const int split_lds = g.wv_lds + 2 * g.wv_split_buf + 2 * 64 * (occ ? g.wlen / 2 : g.wlen) +
-                          (MAPFX_SPLIT_ALT ? SPLIT_FOLD_LDS : 0);
+                          (MAPFX_SPLIT_ALT ? SPLIT_FOLD_LDS : 0) + (MAPFX_SPLIT_MOVE ? SPLIT_RING_LDS : 0);
     const bool split = MAPFX_SPLIT && runner && fullw && g.L == 16 && g.wv_split_buf > 0 &&
                        split_lds <= 64 * 1024 && (al16 & 15) == 0;
     KernelFn fn = pick_wave_kernel((a.obs_window || occ) ? g.window : 0, roll, fullw, runner, g.L, split, occ);

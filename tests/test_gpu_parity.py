@@ -312,6 +312,48 @@ def test_runner_rollout_every_step(mapfx_mod, E, T, win, autoreset, N):
     assert np.array_equal(_np(b1.t), _np(b2.t))
 
 
+@pytest.mark.parametrize("autoreset", [False, True])
+def test_runner_rollout_agents_on_obstacles(mapfx_mod, autoreset):
+    """The store-wave kernel runs the dynamics from static obstacle flags only in blocks
+    where no agent stands (or is reset) on an obstacle; a block with such an agent
+    (quirk 1: the obstacle becomes enterable while occupied) takes the one-wave step
+    side.  Mixed blocks, every step equal to single step launches."""
+    from mapfx.maps import synthetic_instances
+    E, S, N, T, win = 256, 8, 16, 40, 5
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.15, seed=31)
+    bits = np.asarray(inst["bits"])
+    init = np.array(inst["init_pos"])
+    rng = np.random.default_rng(3)
+    for e in range(0, E, 3):          # every third env: one agent starts on an obstacle
+        b_ = bits[e if bits.shape[0] > 1 else 0]
+        cells = [c for c in range(S * S) if (b_[c >> 3] >> (c & 7)) & 1]
+        if cells:
+            c = int(rng.choice(cells))
+            init[e, int(rng.integers(N))] = (c // S, c % S)
+    kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=2000 if not autoreset else 9,
+              obs=("window",), window=win)
+    b1 = mapfx_mod.MapfGridBatch(init, inst["goals"], **kw)
+    b2 = mapfx_mod.MapfGridBatch(init, inst["goals"], **kw)
+    b1.reset()
+    b2.reset()
+    acts = b2.gen_actions(T, 23, t0=0)
+    traj = b1.rollout(T, actions=acts, autoreset=autoreset)
+    for k in range(T):
+        out = b2.step(acts[k])
+        for key in ("reward", "term", "node", "edge", "avail", "obs_window"):
+            x, y = _np(out[key]), _np(traj[key][k])
+            if x.dtype == np.float64:
+                assert np.array_equal(_u64(x), _u64(y)), (key, k)
+            else:
+                assert np.array_equal(x, y), (key, k)
+        assert np.array_equal(_np(traj["traj_pos"][k]), _np(b2.pos)), k
+        assert np.array_equal(_np(traj["traj_done"][k]), _np(b2.done)), k
+        if autoreset and out["term"].any():
+            b2.reset(env_mask=out["term"].clone())
+    assert np.array_equal(_np(b1.pos), _np(b2.pos))
+    assert np.array_equal(_np(b1.t), _np(b2.t))
+
+
 def test_rollout_matches_oracle_long_horizon(mapfx_mod):
     """C2 shape (32x32, 16 agents, 4096 envs), 64 fused steps vs the C oracle."""
     from mapfx.maps import synthetic_instances

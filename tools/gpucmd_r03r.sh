@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 3: plain stores, T sweep, four-wave (nt0) vs three-wave (nt0m0) split.
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out/r03r
+mkdir -p $OUT
+for v in _nt0 _nt0m0; do
+  for T in 1 2 5 10 20 40 64; do
+    MAPFX_LIB=$PWD/mapf-marl_amd/mapfx/libmapfx$v.so timeout -k 10 120 python3 bench.py --gpus 1 --steps $T --warmup $T \
+      --cpu-seconds 0 --per-step-steps 0 > $OUT/c2$v.T$T.json 2>$OUT/c2$v.T$T.err || exit $?
+    python3 -c "import json; d=json.load(open('$OUT/c2$v.T$T.json')); print('lib$v T$T', d['kernel_ms_per_launch'], d['timing']['kernel_ms_replays'])"
+  done
+done
+echo "[$(date +%T)] done"

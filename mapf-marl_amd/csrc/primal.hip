@@ -47,7 +47,6 @@ struct QGeo {
   int hw, bits_words, lut_n;
   int lw, lw_shift, wreg;  // lanes per world (16 / 32 / 64), log2, LDS bytes per world
   int P, PW, rows;         // padded byte map: rows x PW, interior at (P, P); P >= max(1, s / 2)
-  int pws;                 // log2(PW) when PW is a power of two (required by the compile-time-S kernels), else -1
   int off_bm, off_goals, off_ag, off_pair, off_pend, off_rst, off_fst;  // regions of a world
   int diag, nact, apl;     // DIAGONAL_MOVEMENT, actions (5 / 9), agents per lane
   uint64_t m_s, m_ss;      // fastdiv magics (odd s path)
@@ -188,21 +187,9 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
     lom[rr] = nlow >= 4 ? ~0u : (1u << (8 * nlow)) - 1u;
   }
   const bool probe = ag >= 1 && ag <= NDIR;
-  const int pofs = probe ? dir_r(ag) * PW + dir_c(ag) : 0;  // (negative rows: multiply, not shift)
+  const int pofs = probe ? dir_r(ag) * PW + dir_c(ag) : 0;
 
   const long long e0k = (long long)e * a.K;
-  // padded-map row offsets: a shift when the pitch is a power of two (the host picks
-  // one for the compile-time-S kernels), else a multiply
-  const auto rowo = [&](int r) { return S_ ? (r << g.pws) : r * PW; };
-  // the call's move inputs, read one call ahead: aid's record and its target cell
-  // (issued after the previous call's map / record writes: LDS is in order per wave,
-  // so they see them -- also when the same agent acts twice in a row)
-  const auto fetch_move = [&](int2 pr, int4& A, uint32_t& tv) {
-    const int id = min(max(pr.x - 1, 0), N - 1);
-    const int ac = (uint32_t)pr.y < 9u ? pr.y : 0;
-    A = agL[id];
-    tv = cm[rowo(A.x + dir_r(ac) + P) + A.y + dir_c(ac) + P];  // |d| <= 1 <= P: inside
-  };
   int kstop = live ? a.K : 0;  // calls of this world from kstop on are not run (bad call)
   for (int kb = 0; kb < a.K; kb += 64) {
     const int kend = min(a.K, kb + 64);
@@ -212,12 +199,7 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
       for (int j = ag; j < kend - kb; j += lw) pairL[j] = make_int2(a.ids[e0k + kb + j], a.acts[e0k + kb + j]);
     wave_fence();
     int2 pa = pairL[0];
-    int4 A;
-    uint32_t tv;
-    fetch_move(pa, A, tv);
-    uint8_t* const oblk = a.obs ? a.obs + (e0k + kb) * 4 * ss : nullptr;  // the block's records
-    uint32_t ooff = 0;                                                    // call k's: (k - kb) 4 s^2
-    for (int k = kb; k < kend; ++k, ooff += 4 * ss) {
+    for (int k = kb; k < kend; ++k) {
       const int2 nxt = pairL[min(k + 1 - kb, 63)];  // the next call's pair, read ahead
       const int aid = pa.x - 1, act = pa.y;
       pa = nxt;
@@ -228,8 +210,10 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
         continue;
       }
       // ---- State.moveAgent (:103-135), resolved by every lane of the world ----
+      const int4 A = agL[aid];  // broadcast read: aid's (row, col, goal row, goal col)
       const int nx = A.x + dir_r(act), ny = A.y + dir_c(act);
       const bool inb = nx < H && nx >= 0 && ny < W && ny >= 0;
+      const uint32_t tv = cm[(nx + P) * PW + ny + P];  // |d| <= 1 <= P: inside the padded map
       bool dcol = false;
       if constexpr (DIAG) {  // diagonalCollision (:77-99) against the PRE-move positions
         const int sx = A.x + nx, sy = A.y + ny;
@@ -245,11 +229,10 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
       const int st_blocked = !inb ? -1 : (wall ? -2 : -3);  // out of bounds, wall, robot / diagonal
       const int status = act == 0 ? (on_old ? 1 : 0) : (moved ? (on_new ? 1 : (on_old ? 2 : 0)) : st_blocked);
       const int cx = moved ? nx : A.x, cy = moved ? ny : A.y;
-      const int gx0 = A.z, gy0 = A.w;
       ngoal += (moved && on_new ? 1 : 0) - (moved && on_old ? 1 : 0);
       if (moved && ag == 0) {
-        cm[rowo(A.x + P) + A.y + P] = 0;
-        cm[rowo(nx + P) + ny + P] = 1;
+        cm[(A.x + P) * PW + A.y + P] = 0;
+        cm[(nx + P) * PW + ny + P] = 1;
         *(int2*)&agL[aid] = make_int2(nx, ny);
       }
 #pragma unroll
@@ -262,14 +245,13 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
         }
       }
       wave_fence();
-      fetch_move(nxt, A, tv);  // the next call's move inputs (after this call's writes)
       // ---- _observe (:343-386) on the post-move world, next valid actions ----
       const int tr = cx - h2, tc = cy - h2;
-      const int base = rowo(tr + P) + tc + P;  // first window cell in the padded map
-      const int gq = (gx0 >= tr && gx0 < tr + s && gy0 >= tc && gy0 < tc + s)
-                         ? (gx0 - tr) * s + (gy0 - tc) : -(1 << 20);  // own goal's window cell
+      const int base = (tr + P) * PW + tc + P;  // first window cell in the padded map
+      const int gq = (A.z >= tr && A.z < tr + s && A.w >= tc && A.w < tc + s)
+                         ? (A.z - tr) * s + (A.w - tc) : -(1 << 20);  // own goal's window cell
       uint32_t V[RW];
-      if (a.obs && even) {  // (a.obs: a uniform test)
+      if (a.obs && even) {
 #pragma unroll
         for (int rr = 0; rr < RW; ++rr) {
           V[rr] = 0;
@@ -281,10 +263,8 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
           }
         }
       }
-      // _listNextValidActions (:639-667): lane d probes action d (others read their own
-      // cell, discarded): in bounds, no wall, no robot
-      const bool free_nb = cm[base + rowo(h2) + h2 + pofs] == 0;  // every lane reads (no branch)
-      const bool ok = probe & free_nb;
+      bool ok = false;  // _listNextValidActions (:639-667): lane d probes action d
+      if (probe) ok = cm[(cx + P) * PW + cy + P + pofs] == 0;  // in bounds, no wall, no robot
       uint32_t dmask = 0;  // DIAG: directions refused by diagonalCollision from (cx, cy)
 #pragma unroll
       for (int r = 0; r < MA; ++r) {
@@ -309,7 +289,7 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
       if (opp > 0) mask &= ~(1u << opp);
       wave_fence();
       if (a.obs) {
-        uint8_t* o = oblk + ooff;
+        uint8_t* o = a.obs + (e0k + k) * 4 * ss;
         if (even) {
 #pragma unroll
           for (int rr = 0; rr < RW; ++rr) {
@@ -335,7 +315,7 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
               const int b = 4 * m + t;
               const int pl = fdiv(b, g.m_ss), i = b - pl * ss;
               const int y = fdiv(i, g.m_s), x = i - y * s;
-              const uint32_t v = cm[base + rowo(y) + x];
+              const uint32_t v = cm[base + y * PW + x];
               uint32_t bv;
               if (pl == 0) bv = v & 1u;
               else if (pl == 1) bv = i == gq ? 1u : 0u;
@@ -356,11 +336,11 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
         const int j = k - kb;
         rst[j] = rew;
         fst[j] = ngoal == N ? 1 : 0;                          // world.done() (:626)
-        fst[64 + j] = (cx == gx0 && cy == gy0) ? 1 : 0;       // on_goal (:633)
+        fst[64 + j] = (cx == A.z && cy == A.w) ? 1 : 0;       // on_goal (:633)
         fst[128 + j] = status >= 0 ? 1 : 0;                   // valid_action (:566)
         fst[192 + j] = (uint8_t)mask;
         if constexpr (DIAG) fst[256 + j] = (uint8_t)(mask >> 8);
-        pend[j] = make_int2(gx0 - cx, gy0 - cy);              // goal vector (:379-384), LUT later
+        pend[j] = make_int2(A.z - cx, A.w - cy);              // goal vector (:379-384), LUT later
       }
     }
     wave_fence();
@@ -436,8 +416,7 @@ PrimalFn pick_ls(int ls, int apl) {
   return pick_ma<S, 6, DIAG>(apl);
 }
 PrimalFn pick_primal(const QGeo& g) {
-  if (g.s == 10 && g.pws >= 0)
-    return g.diag ? pick_ls<10, true>(g.lw_shift, g.apl) : pick_ls<10, false>(g.lw_shift, g.apl);
+  if (g.s == 10) return g.diag ? pick_ls<10, true>(g.lw_shift, g.apl) : pick_ls<10, false>(g.lw_shift, g.apl);
   return g.diag ? pick_ls<0, true>(g.lw_shift, g.apl) : pick_ls<0, false>(g.lw_shift, g.apl);
 }
 
@@ -496,12 +475,6 @@ int mapfx_primal_create(const mapfx_primal_cfg* cfg, mapfx_primal_t** out) {
   g.P = std::max(1, g.s / 2);
   g.PW = (c.W + 2 * g.P + 3) & ~3;
   g.rows = c.H + 2 * g.P;
-  g.pws = -1;
-  {  // a power-of-two pitch (row offsets by shifts) while it costs at most 2x the map
-    int p2 = 4, sh = 2;
-    while (p2 < g.PW) p2 <<= 1, ++sh;
-    if (p2 <= 2 * g.PW && g.rows * p2 <= 32 * 1024) g.PW = p2, g.pws = sh;
-  }
   g.m_s = magic48(g.s);
   g.m_ss = magic48(g.s * g.s);
   const int wreg = layout(g);

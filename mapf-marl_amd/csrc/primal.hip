@@ -50,6 +50,8 @@ struct QGeo {
   int off_bm, off_goals, off_ag, off_pair, off_pend, off_rst, off_fst;  // regions of a world
   int diag, nact, apl;     // DIAGONAL_MOVEMENT, actions (5 / 9), agents per lane
   uint64_t m_s, m_ss;      // fastdiv magics (odd s path)
+  // primal_seq_kernel (world per wave): LDS regions and size; seq = 0 when not eligible
+  int seq, off_gl, off_snap, off_psnap, off_bstr, lds_seq;
 };
 
 struct QArgs {
@@ -381,6 +383,295 @@ __global__ void __launch_bounds__(64) primal_act_kernel(QGeo g, QArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// primal_seq_kernel<S, DIAG>: one world per wave, the calls of a 64-call block in two
+// phases (even s in 4..10, N <= 64, H + 2P <= 64, W + 2P <= 64).
+//
+// The only truly sequential part of _step is State.moveAgent (:103-135): whether call
+// k's move happens depends on the positions the earlier calls left.  Everything else a
+// call returns (_observe :343-386, done :159-166, _listNextValidActions :639-667, the
+// reward :579-596) is a function of the positions right after the call.  So:
+//
+//   phase A (the chain, wave-uniform, no LDS on it): lane j holds agent j's position;
+//     per call the moved agent's position and the target row's wall mask are
+//     v_readlane'd, the robot test is a ballot of lane compares (DIAG: the midpoint
+//     test of diagonalCollision :77-99 is a second ballot), the move is a v_cndmask
+//     on lane aid.  The call leaves its (old position, moved) in lane k of a log
+//     register and every agent's post-call position in a [64][N] u16 LDS snapshot;
+//   phase B (parallel, lane k = call k): each lane rebuilds its call's status, reward,
+//     done, next-action mask and goal vector from the log and the snapshot, and its
+//     call's four observation planes as four S*S-bit masks (walls from padded row
+//     masks, agents and clamped goals set bit by bit from the snapshot); the 4*S*S-bit
+//     string of call k goes to LDS, and the wave expands strings to bytes (one bit ->
+//     one byte, 16 bits per lane-chunk) and writes the block's records as one
+//     contiguous run of 16-byte stores.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// acc |= bit idx (idx < 128; 127 is the "nothing" sentinel, masked off later)
+__device__ __forceinline__ void set_bit128(uint32_t (&acc)[4], uint32_t idx) {
+  const uint32_t b = 1u << (idx & 31u), w = idx >> 5;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] |= (w == (uint32_t)i) ? b : 0u;
+}
+
+// str |= v at compile-time bit offset B (v has no bits at or above `bits`)
+template <int B, int NSW>
+__device__ __forceinline__ void put_at(uint32_t (&str)[NSW], uint32_t v) {
+  constexpr int w = B >> 5, sh = B & 31;
+  if constexpr (w < NSW) str[w] |= v << sh;
+  if constexpr (sh != 0 && w + 1 < NSW) str[w + 1] |= v >> (32 - sh);
+}
+
+template <int P0, int SS, int NSW>
+__device__ __forceinline__ void put_plane(uint32_t (&str)[NSW], const uint32_t (&pl)[4]) {
+  put_at<P0, NSW>(str, SS >= 32 ? pl[0] : (pl[0] & ((1u << (SS & 31)) - 1u)));
+  if constexpr (SS > 32) put_at<P0 + 32, NSW>(str, SS >= 64 ? pl[1] : (pl[1] & ((1u << (SS & 31)) - 1u)));
+  if constexpr (SS > 64) put_at<P0 + 64, NSW>(str, SS >= 96 ? pl[2] : (pl[2] & ((1u << (SS & 31)) - 1u)));
+  if constexpr (SS > 96) put_at<P0 + 96, NSW>(str, pl[3] & ((1u << (SS & 31)) - 1u));
+}
+
+template <int S, bool DIAG>
+__global__ void __launch_bounds__(64) primal_seq_kernel(QGeo g, QArgs a) {
+  extern __shared__ __align__(16) unsigned char lds[];
+  constexpr int SS = S * S, H2 = S / 2;
+  constexpr int CPC = SS / 4;              // 16-byte chunks of one call's 4 S^2-byte record
+  constexpr int NSW = (4 * SS + 31) / 32;  // dwords of a call's bit string (slot: 16 dwords)
+  constexpr int NDIR = DIAG ? 8 : 4;
+  static_assert(S % 2 == 0 && S >= 4 && SS <= 100, "even S in 4..10");
+  const int lane = threadIdx.x, e = blockIdx.x;
+  const int N = g.N, H = g.H, W = g.W, P = g.P;
+  uint64_t* rowm = (uint64_t*)lds;                          // [H + 2P] padded wall rows
+  uint32_t* gl = (uint32_t*)(lds + g.off_gl);               // [N] goal row | col << 16
+  uint16_t* snap = (uint16_t*)(lds + g.off_snap);           // [64][N] row | col << 8 after call k
+  uint16_t* psnap = (uint16_t*)(lds + g.off_psnap);         // DIAG: agents_past after call k
+  uint32_t* bstr = (uint32_t*)(lds + g.off_bstr);           // [64][16] bit strings of the calls
+
+  // ---- state: lane j = agent j (row | col << 16); other lanes never match a cell ----
+  const bool agent = lane < N;
+  uint32_t vpos = 0xFFFFFFFFu, vpast = 0u;
+  if (agent) {
+    const long long i = (long long)e * N + lane;
+    const int2 p = ((const int2*)a.pos)[i], q = ((const int2*)a.goal)[i];
+    vpos = (uint32_t)p.x | ((uint32_t)p.y << 16);
+    gl[lane] = (uint32_t)q.x | ((uint32_t)q.y << 16);
+    if constexpr (DIAG) {
+      const int2 pp = ((const int2*)a.past)[i];
+      vpast = (uint32_t)pp.x | ((uint32_t)pp.y << 16);
+    }
+  }
+  uint32_t vsum = vpos + vpast;  // DIAG: past + present, the midpoint test's sum (sentinel off-agent)
+  // ---- padded wall rows: lane r = padded row r, bit c + P = wall at column c; outside = 1 ----
+  uint64_t vrow = ~0ull;
+  {
+    const int r = lane - P;
+    if (r >= 0 && r < H) {
+      const uint32_t* w32 = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)e * g.map_stride));
+      const int b0 = r * W, wi = b0 >> 5, sh = b0 & 31, last = (b0 + W - 1) >> 5;
+      const uint64_t d0 = w32[wi], d1 = wi + 1 <= last ? w32[wi + 1] : 0u, d2 = wi + 2 <= last ? w32[wi + 2] : 0u;
+      uint64_t v = (d0 | (d1 << 32)) >> sh;
+      if (sh) v |= d2 << (64 - sh);
+      const uint64_t fm = ((1ull << W) - 1ull) << P;
+      vrow = (~fm) | ((v << P) & fm);
+    }
+    if (lane < H + 2 * P) rowm[lane] = vrow;
+  }
+  const uint32_t vrow_lo = (uint32_t)vrow, vrow_hi = (uint32_t)(vrow >> 32);
+  wave_fence();
+
+  const long long e0k = (long long)e * a.K;
+  int kstop = a.K;
+  for (int kb = 0; kb < kstop; kb += 64) {
+    const int nb = min(64, a.K - kb);
+    // (agent index, action) of call kb + lane, or a sentinel for a bad call (:556-558)
+    uint32_t vpair = 0xFFFFFFFFu;
+    if (lane < nb) {
+      const int id = a.ids[e0k + kb + lane], ac = a.acts[e0k + kb + lane];
+      if ((unsigned)(id - 1) < (unsigned)N && (unsigned)ac < (unsigned)g.nact)
+        vpair = (uint32_t)(id - 1) | ((uint32_t)ac << 8);
+    }
+    // ================= phase A: State.moveAgent, call after call =================
+    uint32_t vlog = 0;
+    int nv = nb;
+    for (int kk = 0; kk < nb; ++kk) {
+      const uint32_t pr = readlane_u32(vpair, kk);
+      if (pr == 0xFFFFFFFFu) {
+        nv = kk;
+        break;
+      }
+      const int aid = (int)(pr & 0xFFu), act = (int)(pr >> 8);
+      const uint32_t o = readlane_u32(vpos, aid);
+      const int nx = (int)(o & 0xFFFFu) + dir_r(act), ny = (int)(o >> 16) + dir_c(act);
+      const bool inb = (unsigned)nx < (unsigned)H && (unsigned)ny < (unsigned)W;
+      const int rs = nx + P;  // P - 1 .. H + P: a padded row
+      const uint64_t wr = ((uint64_t)readlane_u32(vrow_hi, rs) << 32) | readlane_u32(vrow_lo, rs);
+      const bool wall = ((wr >> (ny + P)) & 1ull) != 0;
+      const uint32_t t = (uint32_t)(nx & 0xFFFF) | ((uint32_t)ny << 16);
+      const bool robot = __ballot(vpos == t) != 0;
+      bool dcol = false;
+      if constexpr (DIAG) dcol = __ballot(vsum == o + t && lane != aid) != 0;
+      const bool moved = act != 0 && inb && !wall && !robot && !dcol;
+      if (lane == aid) {
+        if constexpr (DIAG) {
+          if (act == 0 || moved) vpast = o;  // agents_past (:110-112, :129-131)
+        }
+        if (moved) vpos = t;
+        vsum = vpos + vpast;
+      }
+      if (lane == kk) vlog = o | (moved ? 0x80000000u : 0u);
+      if (agent) {
+        snap[kk * N + lane] = (uint16_t)((vpos & 0xFFu) | ((vpos >> 8) & 0xFF00u));
+        if constexpr (DIAG) psnap[kk * N + lane] = (uint16_t)((vpast & 0xFFu) | ((vpast >> 8) & 0xFF00u));
+      }
+    }
+    if (nv < nb) {  // the reference asserts (:556-558): this world runs no further call
+      if (lane == 0 && a.err) atomicCAS(a.err, 0, e + 1);
+      kstop = kb + nv;
+    }
+    wave_fence();
+    // ================= phase B: lane k = call kb + k =================
+    const bool cv = lane < nv;
+    const int aid = cv ? (int)(vpair & 0xFFu) : 0, act = cv ? (int)((vpair >> 8) & 0xFFu) : 0;
+    const uint32_t o = vlog & 0x7FFFFFFFu;
+    const bool moved = (vlog >> 31) != 0;
+    const int ox = (int)(o & 0xFFFFu), oy = (int)(o >> 16);
+    const int nx = ox + dir_r(act), ny = oy + dir_c(act);
+    const bool inb = (unsigned)nx < (unsigned)H && (unsigned)ny < (unsigned)W;
+    const int cx = moved ? nx : ox, cy = moved ? ny : oy;
+    const uint32_t gA = gl[aid];
+    const int gx = (int)(gA & 0xFFFFu), gy = (int)(gA >> 16);
+    const int tr = cx - H2, tc = cy - H2;
+    // obstacle plane (:356-362, outside = 1) and the walls of the 3 x 3 around (cx, cy)
+    uint32_t obsp[4] = {0u, 0u, 0u, 0u};
+    uint32_t w9 = 0;
+#pragma unroll
+    for (int y = 0; y < S; ++y) {
+      const uint64_t m = rowm[tr + y + P];
+      const uint32_t bits = (uint32_t)(m >> (tc + P)) & ((1u << S) - 1u);
+      const int B = S * y;
+      obsp[B >> 5] |= bits << (B & 31);
+      if ((B & 31) + S > 32) obsp[(B >> 5) + 1] |= bits >> (32 - (B & 31));
+      if (y >= H2 - 1 && y <= H2 + 1) w9 |= ((bits >> (H2 - 1)) & 7u) << (3 * (y - H2 + 1));
+    }
+    // agents at this call: poss plane (:363-372), visible agents' clamped goals (:374-378),
+    // agents on goal (done), occupied neighbours (next actions), DIAG crossing directions
+    uint32_t possp[4] = {0u, 0u, 0u, 0u}, goalsp[4] = {0u, 0u, 0u, 0u};
+    uint32_t nb9 = 0, dmask = 0;
+    int ngoal = 0;
+    const uint16_t* sk = snap + lane * N;
+    const uint16_t* pk = psnap + lane * N;
+    for (int j = 0; j < N; ++j) {
+      const uint32_t pj = sk[j], gj = gl[j];
+      const int jx = (int)(pj & 0xFFu), jy = (int)(pj >> 8);
+      const int gjx = (int)(gj & 0xFFFFu), gjy = (int)(gj >> 16);
+      ngoal += (jx == gjx && jy == gjy) ? 1 : 0;
+      const int dx = jx - tr, dy = jy - tc;
+      const bool vis = (unsigned)dx < (unsigned)S && (unsigned)dy < (unsigned)S;
+      set_bit128(possp, vis ? (uint32_t)(dx * S + dy) : 127u);
+      const int mx = min(max(gjx - tr, 0), S - 1), my = min(max(gjy - tc, 0), S - 1);
+      set_bit128(goalsp, (vis && j != aid) ? (uint32_t)(mx * S + my) : 127u);
+      const int ex = jx - cx + 1, ey = jy - cy + 1;
+      if ((unsigned)ex < 3u && (unsigned)ey < 3u) nb9 |= 1u << (ex * 3 + ey);
+      if constexpr (DIAG) {
+        const uint32_t qj = pk[j];
+        const int sx = (int)(qj & 0xFFu) + jx - 2 * cx, sy = (int)(qj >> 8) + jy - 2 * cy;
+        if (j != aid && sx >= -1 && sx <= 1 && sy >= -1 && sy <= 1)
+          dmask |= 1u << (uint32_t)((ACT_OF >> (4 * ((sx + 1) * 3 + sy + 1))) & 0xFu);
+      }
+    }
+    uint32_t goalp[4] = {0u, 0u, 0u, 0u};
+    {
+      const int dx = gx - tr, dy = gy - tc;
+      set_bit128(goalp, ((unsigned)dx < (unsigned)S && (unsigned)dy < (unsigned)S) ? (uint32_t)(dx * S + dy) : 127u);
+    }
+    // status (State.moveAgent), reward (:579-596), next valid actions (:639-667)
+    const bool on_old = gx == ox && gy == oy, on_new = gx == nx && gy == ny;
+    const int i9 = (dir_r(act) + 1) * 3 + dir_c(act) + 1;  // target cell in the 3 x 3 (when not moved, c = o)
+    const bool wallT = ((w9 >> i9) & 1u) != 0;
+    const int st_blocked = !inb ? -1 : (wallT ? -2 : -3);
+    const int status = act == 0 ? (on_old ? 1 : 0) : (moved ? (on_new ? 1 : (on_old ? 2 : 0)) : st_blocked);
+    const uint32_t blocked9 = w9 | nb9;
+    uint32_t mask = 1u;
+#pragma unroll
+    for (int d = 1; d <= NDIR; ++d) {
+      const int id9 = (dir_r(d) + 1) * 3 + dir_c(d) + 1;
+      mask |= ((~blocked9 >> id9) & 1u) << d;
+    }
+    const int opp = opposite(act);
+    if (opp > 0) mask &= ~(1u << opp);
+    if constexpr (DIAG) mask &= ~(dmask & 0x1FEu);
+    if (cv) {
+      const long long oi = e0k + kb + lane;
+      const double rew = act == 0 ? (status == 1 ? GOAL_REWARD + 0 : IDLE_COST)
+                                  : status == 1 ? GOAL_REWARD : status < 0 ? COLLISION_REWARD : ACTION_COST;
+      if (a.reward) a.reward[oi] = rew;
+      if (a.done) a.done[oi] = ngoal == N ? 1 : 0;
+      if (a.on_goal) a.on_goal[oi] = (cx == gx && cy == gy) ? 1 : 0;
+      if (a.valid) a.valid[oi] = status >= 0 ? 1 : 0;
+      if (a.next_mask) {
+        if constexpr (DIAG) ((uint16_t*)a.next_mask)[oi] = (uint16_t)mask;
+        else a.next_mask[oi] = (uint8_t)mask;
+      }
+      if (a.vec) {  // :379-386, magnitude from the host libm pow LUT
+        const int dX = gx - cx, dY = gy - cy;
+        const double mag = a.pow_lut[dX * dX + dY * dY];
+        double vx = (double)dX, vy = (double)dY;
+        if (mag != 0.0) {
+          vx = vx / mag;
+          vy = vy / mag;
+        }
+        double* v = a.vec + oi * 3;
+        v[0] = vx;
+        v[1] = vy;
+        v[2] = mag;
+      }
+    }
+    if (a.obs) {
+      uint32_t str[NSW];
+#pragma unroll
+      for (int i = 0; i < NSW; ++i) str[i] = 0u;
+      put_plane<0, SS, NSW>(str, possp);
+      put_plane<SS, SS, NSW>(str, goalp);
+      put_plane<2 * SS, SS, NSW>(str, goalsp);
+      put_plane<3 * SS, SS, NSW>(str, obsp);
+      uint32_t* dst = bstr + lane * 16;
+#pragma unroll
+      for (int i = 0; i < NSW; i += 4) {
+        uint4 v;
+        v.x = str[i];
+        v.y = i + 1 < NSW ? str[i + 1] : 0u;
+        v.z = i + 2 < NSW ? str[i + 2] : 0u;
+        v.w = i + 3 < NSW ? str[i + 3] : 0u;
+        *(uint4*)(dst + i) = v;
+      }
+      wave_fence();
+      // the block's records are one contiguous run: 16-byte chunk c = bits 16q .. 16q + 15
+      // of call c / CPC's string (q = c % CPC), one bit per byte
+      const uint16_t* b16 = (const uint16_t*)bstr;
+      uint4* ob = (uint4*)(a.obs + (e0k + kb) * (4 * SS));
+      const int nch = nv * CPC;
+      for (int c = lane; c < nch; c += 64) {
+        const int k = c / CPC, q = c - k * CPC;
+        const uint32_t b = b16[k * 32 + q];
+        uint4 v;
+        v.x = ((b & 15u) * 0x00204081u) & 0x01010101u;
+        v.y = (((b >> 4) & 15u) * 0x00204081u) & 0x01010101u;
+        v.z = (((b >> 8) & 15u) * 0x00204081u) & 0x01010101u;
+        v.w = ((b >> 12) * 0x00204081u) & 0x01010101u;
+        ob[c] = v;
+      }
+    }
+    wave_fence();
+  }
+  if (agent) {
+    const long long i = (long long)e * N + lane;
+    ((int2*)a.pos)[i] = make_int2((int)(vpos & 0xFFFFu), (int)(vpos >> 16));
+    if constexpr (DIAG) ((int2*)a.past)[i] = make_int2((int)(vpast & 0xFFFFu), (int)(vpast >> 16));
+  }
+}
+
 int perr(int code, const char* msg) { return mapfx_internal_error(code, msg); }
 
 int check_hip(hipError_t err, const char* what) {
@@ -395,7 +686,7 @@ int check_hip(hipError_t err, const char* what) {
 }  // namespace
 
 struct mapfx_primal_t {
-  QGeo geo;
+  QGeo geo;  // (seq layout included)
   double* pow_lut;
   int lds;
 };
@@ -422,6 +713,34 @@ PrimalFn pick_primal(const QGeo& g) {
 
 uint64_t magic48(int d) { return ((1ull << 48) + (uint64_t)d - 1) / (uint64_t)d; }
 int r16(int x) { return (x + 15) & ~15; }
+
+template <bool DIAG>
+PrimalFn pick_seq_s(int s) {
+  if (s == 4) return primal_seq_kernel<4, DIAG>;
+  if (s == 6) return primal_seq_kernel<6, DIAG>;
+  if (s == 8) return primal_seq_kernel<8, DIAG>;
+  return primal_seq_kernel<10, DIAG>;
+}
+PrimalFn pick_seq(const QGeo& g) { return g.diag ? pick_seq_s<true>(g.s) : pick_seq_s<false>(g.s); }
+
+// primal_seq_kernel eligibility and LDS layout of its one world per block: padded wall
+// rows (u64), goals (u32), the [64][N] u16 position (and DIAG past) snapshots, the
+// [64][16] u32 bit strings.  Returns the size, 0 when the world does not qualify.
+int layout_seq(QGeo& g) {
+  const bool ok = g.s % 2 == 0 && g.s >= 4 && g.s <= 10 && g.N <= 64 && g.H + 2 * g.P <= 64 &&
+                  g.W + 2 * g.P <= 64;
+  if (!ok) return 0;
+  int o = r16((g.H + 2 * g.P) * 8);
+  g.off_gl = o;
+  o += r16(4 * g.N);
+  g.off_snap = o;
+  o += r16(64 * 2 * g.N);
+  g.off_psnap = o;
+  if (g.diag) o += r16(64 * 2 * g.N);
+  g.off_bstr = o;
+  o += 64 * 64;
+  return o;
+}
 
 // LDS layout of one world for lanes-per-world 1 << ls; returns its size.
 int layout(QGeo& g) {
@@ -477,6 +796,15 @@ int mapfx_primal_create(const mapfx_primal_cfg* cfg, mapfx_primal_t** out) {
   g.rows = c.H + 2 * g.P;
   g.m_s = magic48(g.s);
   g.m_ss = magic48(g.s * g.s);
+  // One world per wave, phase A / phase B (primal_seq_kernel) wherever it applies, unless
+  // a test pins the lane-group kernel (MAPFX_PRIMAL_LANES, or MAPFX_PRIMAL_PATH=groups).
+  {
+    const char* lanes = getenv("MAPFX_PRIMAL_LANES");
+    const char* path = getenv("MAPFX_PRIMAL_PATH");
+    const bool pinned = (lanes && *lanes) || (path && strcmp(path, "groups") == 0);
+    g.lds_seq = pinned ? 0 : layout_seq(g);
+    g.seq = g.lds_seq > 0 ? 1 : 0;
+  }
   const int wreg = layout(g);
   // Lanes per world: the smallest of 16 / 32 / 64 that writes an even-s call's planes
   // in at most 4 rounds (s * s / 4 dwords per plane) and holds the agents in at most
@@ -564,6 +892,10 @@ int mapfx_primal_act(mapfx_primal_t* h, const mapfx_primal_state* st, const int3
     a.err = out->err;
   }
   const QGeo& g = h->geo;
+  if (g.seq && ((uintptr_t)a.obs & 15u) == 0) {  // (16-byte record runs)
+    hipLaunchKernelGGL(pick_seq(g), dim3(g.E), dim3(64), g.lds_seq, (hipStream_t)stream, g, a);
+    return check_hip(hipGetLastError(), "primal_seq_kernel launch");
+  }
   const int wpw = 64 >> g.lw_shift;
   hipLaunchKernelGGL(pick_primal(g), dim3((g.E + wpw - 1) / wpw), dim3(64), h->lds, (hipStream_t)stream, g, a);
   return check_hip(hipGetLastError(), "primal_act_kernel launch");

@@ -79,6 +79,14 @@ void mapfx_primal_destroy(mapfx_primal_t* h);
 int mapfx_primal_act(mapfx_primal_t* h, const mapfx_primal_state* st, const int32_t* agent_ids,
                      const int32_t* actions, int32_t K, const mapfx_primal_out* out, void* stream);
 
+/* mapfx_primal_act with the launch's own start / stop timestamps recorded into
+ * `start_event` / `stop_event` (hipEvent_t, created by the caller) at the kernel's
+ * begin and end (hipExtLaunchKernel): the kernel duration, without the host's
+ * launch gaps.  NULL events: plain mapfx_primal_act. */
+int mapfx_primal_act_timed(mapfx_primal_t* h, const mapfx_primal_state* st, const int32_t* agent_ids,
+                           const int32_t* actions, int32_t K, const mapfx_primal_out* out,
+                           void* start_event, void* stop_event, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,6 +22,7 @@
 // vector) are staged in LDS and leave once per 64-call block as coalesced runs.
 // The goal-vector magnitude comes from a host libm pow LUT, as the reference
 // computes `(dx**2 + dy**2) ** .5` (quirk 8).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -433,33 +434,39 @@ __device__ __forceinline__ void put_plane(uint32_t (&str)[NSW], const uint32_t (
   if constexpr (SS > 96) put_at<P0 + 96, NSW>(str, pl[3] & ((1u << (SS & 31)) - 1u));
 }
 
+#ifndef MAPFX_QABL
+#define MAPFX_QABL 0  // diagnostic builds only: 1 no record stores, 2 no phase B, 4 no move chain
+#endif
 template <int S, bool DIAG>
 __global__ void __launch_bounds__(64) primal_seq_kernel(QGeo g, QArgs a) {
   extern __shared__ __align__(16) unsigned char lds[];
   constexpr int SS = S * S, H2 = S / 2;
-  constexpr int CPC = SS / 4;              // 16-byte chunks of one call's 4 S^2-byte record
-  constexpr int NSW = (4 * SS + 31) / 32;  // dwords of a call's bit string (slot: 16 dwords)
+  constexpr int CPC = SS / 4;              // 16-byte chunks (= 16-bit string pieces) of one call
+  constexpr int NSW = (4 * SS + 31) / 32;  // dwords of a call's bit string
   constexpr int NDIR = DIAG ? 8 : 4;
   static_assert(S % 2 == 0 && S >= 4 && SS <= 100, "even S in 4..10");
   const int lane = threadIdx.x, e = blockIdx.x;
   const int N = g.N, H = g.H, W = g.W, P = g.P;
-  uint64_t* rowm = (uint64_t*)lds;                          // [H + 2P] padded wall rows
-  uint32_t* gl = (uint32_t*)(lds + g.off_gl);               // [N] goal row | col << 16
-  uint16_t* snap = (uint16_t*)(lds + g.off_snap);           // [64][N] row | col << 8 after call k
-  uint16_t* psnap = (uint16_t*)(lds + g.off_psnap);         // DIAG: agents_past after call k
-  uint32_t* bstr = (uint32_t*)(lds + g.off_bstr);           // [64][16] bit strings of the calls
+  uint64_t* rowm = (uint64_t*)lds;                   // [H + 2P] padded wall rows
+  uint32_t* gl = (uint32_t*)(lds + g.off_gl);        // [N] biased goal (row + P) | (col + P) << 16
+  uint16_t* snap = (uint16_t*)(lds + g.off_snap);    // [64][N] biased row | col << 8 after call k
+  uint16_t* psnap = (uint16_t*)(lds + g.off_psnap);  // DIAG: agents_past after call k
+  uint16_t* bstr = (uint16_t*)(lds + g.off_bstr);    // the block's bit strings, call k at CPC * k
+  const int2* goal2 = (const int2*)a.goal + (long long)e * N;  // wave-uniform reads: SGPRs
 
-  // ---- state: lane j = agent j (row | col << 16); other lanes never match a cell ----
+  // ---- state: lane j = agent j at the BIASED cell (row + P) | (col + P) << 16, which is
+  //      also its padded-map coordinate; other lanes hold a value no cell has ----
   const bool agent = lane < N;
+  const uint32_t bias = (uint32_t)P | ((uint32_t)P << 16);
   uint32_t vpos = 0xFFFFFFFFu, vpast = 0u;
   if (agent) {
     const long long i = (long long)e * N + lane;
-    const int2 p = ((const int2*)a.pos)[i], q = ((const int2*)a.goal)[i];
-    vpos = (uint32_t)p.x | ((uint32_t)p.y << 16);
-    gl[lane] = (uint32_t)q.x | ((uint32_t)q.y << 16);
+    const int2 p = ((const int2*)a.pos)[i], q = goal2[lane];
+    vpos = ((uint32_t)p.x | ((uint32_t)p.y << 16)) + bias;
+    gl[lane] = ((uint32_t)q.x | ((uint32_t)q.y << 16)) + bias;
     if constexpr (DIAG) {
       const int2 pp = ((const int2*)a.past)[i];
-      vpast = (uint32_t)pp.x | ((uint32_t)pp.y << 16);
+      vpast = ((uint32_t)pp.x | ((uint32_t)pp.y << 16)) + bias;
     }
   }
   uint32_t vsum = vpos + vpast;  // DIAG: past + present, the midpoint test's sum (sentinel off-agent)
@@ -485,110 +492,125 @@ __global__ void __launch_bounds__(64) primal_seq_kernel(QGeo g, QArgs a) {
   int kstop = a.K;
   for (int kb = 0; kb < kstop; kb += 64) {
     const int nb = min(64, a.K - kb);
-    // (agent index, action) of call kb + lane, or a sentinel for a bad call (:556-558)
-    uint32_t vpair = 0xFFFFFFFFu;
+    // call kb + lane: agent index, action, and the move as one packed add (cells biased,
+    // so a row step never borrows from the column half); the first bad call ends the
+    // world's calls (the reference asserts, :556-558)
+    bool okc = false;
+    int id = 0, ac = 0;
     if (lane < nb) {
-      const int id = a.ids[e0k + kb + lane], ac = a.acts[e0k + kb + lane];
-      if ((unsigned)(id - 1) < (unsigned)N && (unsigned)ac < (unsigned)g.nact)
-        vpair = (uint32_t)(id - 1) | ((uint32_t)ac << 8);
+      id = a.ids[e0k + kb + lane];
+      ac = a.acts[e0k + kb + lane];
+      okc = (unsigned)(id - 1) < (unsigned)N && (unsigned)ac < (unsigned)g.nact;
     }
+    const uint64_t badm = __ballot(lane < nb && !okc);
+    const int nv = badm ? (int)__ffsll((unsigned long long)badm) - 1 : nb;
+    const int vaid = okc ? id - 1 : 0, vact = okc ? ac : 0;
+    const uint32_t vdel = okc ? (uint32_t)(dir_r(ac) + dir_c(ac) * 65536) : 0u;
     // ================= phase A: State.moveAgent, call after call =================
-    uint32_t vlog = 0;
-    int nv = nb;
-    for (int kk = 0; kk < nb; ++kk) {
-      const uint32_t pr = readlane_u32(vpair, kk);
-      if (pr == 0xFFFFFFFFu) {
-        nv = kk;
-        break;
+    uint32_t vlog = bias;  // (biased (0, 0) for lanes without a call: in-range reads below)
+    // snapshot slots: agent lanes write [kk][lane], the others one spare slot past the rows
+    uint32_t saddr = agent ? 2u * (uint32_t)lane : 2u * 64u * (uint32_t)N;
+    const uint32_t sinc = agent ? 2u * (uint32_t)N : 0u;
+    for (int kk = 0; kk < nv; ++kk) {
+      if (MAPFX_QABL & 4) {
+        *(uint16_t*)((unsigned char*)snap + saddr) = (uint16_t)vpos;
+        saddr += sinc;
+        continue;
       }
-      const int aid = (int)(pr & 0xFFu), act = (int)(pr >> 8);
-      const uint32_t o = readlane_u32(vpos, aid);
-      const int nx = (int)(o & 0xFFFFu) + dir_r(act), ny = (int)(o >> 16) + dir_c(act);
-      const bool inb = (unsigned)nx < (unsigned)H && (unsigned)ny < (unsigned)W;
-      const int rs = nx + P;  // P - 1 .. H + P: a padded row
+      const int aid = __builtin_amdgcn_readlane(vaid, kk);
+      const uint32_t d = readlane_u32(vdel, kk);
+      const uint32_t o = readlane_u32(vpos, aid), t = o + d;
+      const int rs = (int)(t & 0xFFFFu);  // padded row of the target (outside = wall)
       const uint64_t wr = ((uint64_t)readlane_u32(vrow_hi, rs) << 32) | readlane_u32(vrow_lo, rs);
-      const bool wall = ((wr >> (ny + P)) & 1ull) != 0;
-      const uint32_t t = (uint32_t)(nx & 0xFFFF) | ((uint32_t)ny << 16);
-      const bool robot = __ballot(vpos == t) != 0;
-      bool dcol = false;
-      if constexpr (DIAG) dcol = __ballot(vsum == o + t && lane != aid) != 0;
-      const bool moved = act != 0 && inb && !wall && !robot && !dcol;
+      // wall / outside, or an agent on the target (a stay hits itself)
+      uint64_t blk = ((wr >> (t >> 16)) & 1ull) | __ballot(vpos == t);
+      if constexpr (DIAG) blk |= __ballot(vsum == o + t && lane != aid);
+      const bool moved = blk == 0;
       if (lane == aid) {
         if constexpr (DIAG) {
-          if (act == 0 || moved) vpast = o;  // agents_past (:110-112, :129-131)
+          if (d == 0u || moved) vpast = o;  // agents_past (:110-112, :129-131)
         }
         if (moved) vpos = t;
-        vsum = vpos + vpast;
       }
+      if constexpr (DIAG) vsum = vpos + vpast;
       if (lane == kk) vlog = o | (moved ? 0x80000000u : 0u);
-      if (agent) {
-        snap[kk * N + lane] = (uint16_t)((vpos & 0xFFu) | ((vpos >> 8) & 0xFF00u));
-        if constexpr (DIAG) psnap[kk * N + lane] = (uint16_t)((vpast & 0xFFu) | ((vpast >> 8) & 0xFF00u));
-      }
+      const uint16_t sv = (uint16_t)((vpos & 0xFFu) | ((vpos >> 8) & 0xFF00u));
+      *(uint16_t*)((unsigned char*)snap + saddr) = sv;
+      if constexpr (DIAG) *(uint16_t*)((unsigned char*)psnap + saddr) = (uint16_t)((vpast & 0xFFu) | ((vpast >> 8) & 0xFF00u));
+      saddr += sinc;
     }
-    if (nv < nb) {  // the reference asserts (:556-558): this world runs no further call
+    if (nv < nb) {
       if (lane == 0 && a.err) atomicCAS(a.err, 0, e + 1);
       kstop = kb + nv;
     }
     wave_fence();
     // ================= phase B: lane k = call kb + k =================
+    if (MAPFX_QABL & 2) continue;
     const bool cv = lane < nv;
-    const int aid = cv ? (int)(vpair & 0xFFu) : 0, act = cv ? (int)((vpair >> 8) & 0xFFu) : 0;
-    const uint32_t o = vlog & 0x7FFFFFFFu;
+    const int aid = vaid, act = vact;
+    const uint32_t ob = vlog & 0x7FFFFFFFu, tb = ob + vdel;
     const bool moved = (vlog >> 31) != 0;
-    const int ox = (int)(o & 0xFFFFu), oy = (int)(o >> 16);
-    const int nx = ox + dir_r(act), ny = oy + dir_c(act);
-    const bool inb = (unsigned)nx < (unsigned)H && (unsigned)ny < (unsigned)W;
-    const int cx = moved ? nx : ox, cy = moved ? ny : oy;
+    const uint32_t cb = moved ? tb : ob;
+    const int cxb = (int)(cb & 0xFFFFu), cyb = (int)(cb >> 16);
+    const bool inb = (unsigned)((int)(tb & 0xFFFFu) - P) < (unsigned)H && (unsigned)((int)(tb >> 16) - P) < (unsigned)W;
     const uint32_t gA = gl[aid];
-    const int gx = (int)(gA & 0xFFFFu), gy = (int)(gA >> 16);
-    const int tr = cx - H2, tc = cy - H2;
-    // obstacle plane (:356-362, outside = 1) and the walls of the 3 x 3 around (cx, cy)
+    const int gxb = (int)(gA & 0xFFFFu), gyb = (int)(gA >> 16);
+    const int trb = cxb - H2, tcb = cyb - H2;  // window origin in padded coordinates
+    // obstacle plane (:356-362, outside = 1) and the walls of the 3 x 3 around the agent
     uint32_t obsp[4] = {0u, 0u, 0u, 0u};
     uint32_t w9 = 0;
 #pragma unroll
     for (int y = 0; y < S; ++y) {
-      const uint64_t m = rowm[tr + y + P];
-      const uint32_t bits = (uint32_t)(m >> (tc + P)) & ((1u << S) - 1u);
+      const uint64_t m = rowm[trb + y];
+      const uint32_t bits = (uint32_t)(m >> tcb) & ((1u << S) - 1u);
       const int B = S * y;
       obsp[B >> 5] |= bits << (B & 31);
       if ((B & 31) + S > 32) obsp[(B >> 5) + 1] |= bits >> (32 - (B & 31));
       if (y >= H2 - 1 && y <= H2 + 1) w9 |= ((bits >> (H2 - 1)) & 7u) << (3 * (y - H2 + 1));
     }
-    // agents at this call: poss plane (:363-372), visible agents' clamped goals (:374-378),
-    // agents on goal (done), occupied neighbours (next actions), DIAG crossing directions
+    // agents at this call: poss plane (:363-372), visible agents' clamped goals
+    // (:374-378), agents on their goal (done), DIAG crossing directions
     uint32_t possp[4] = {0u, 0u, 0u, 0u}, goalsp[4] = {0u, 0u, 0u, 0u};
-    uint32_t nb9 = 0, dmask = 0;
+    uint32_t dmask = 0;
     int ngoal = 0;
     const uint16_t* sk = snap + lane * N;
     const uint16_t* pk = psnap + lane * N;
     for (int j = 0; j < N; ++j) {
-      const uint32_t pj = sk[j], gj = gl[j];
-      const int jx = (int)(pj & 0xFFu), jy = (int)(pj >> 8);
-      const int gjx = (int)(gj & 0xFFFFu), gjy = (int)(gj >> 16);
-      ngoal += (jx == gjx && jy == gjy) ? 1 : 0;
-      const int dx = jx - tr, dy = jy - tc;
+      const int2 gj = goal2[j];
+      const int gjxb = gj.x + P, gjyb = gj.y + P;
+      const uint32_t pj = sk[j];
+      ngoal += pj == (uint32_t)(gjxb | (gjyb << 8)) ? 1 : 0;
+      const int dx = (int)(pj & 0xFFu) - trb, dy = (int)(pj >> 8) - tcb;
       const bool vis = (unsigned)dx < (unsigned)S && (unsigned)dy < (unsigned)S;
       set_bit128(possp, vis ? (uint32_t)(dx * S + dy) : 127u);
-      const int mx = min(max(gjx - tr, 0), S - 1), my = min(max(gjy - tc, 0), S - 1);
+      const int mx = min(max(gjxb - trb, 0), S - 1), my = min(max(gjyb - tcb, 0), S - 1);
       set_bit128(goalsp, (vis && j != aid) ? (uint32_t)(mx * S + my) : 127u);
-      const int ex = jx - cx + 1, ey = jy - cy + 1;
-      if ((unsigned)ex < 3u && (unsigned)ey < 3u) nb9 |= 1u << (ex * 3 + ey);
       if constexpr (DIAG) {
         const uint32_t qj = pk[j];
-        const int sx = (int)(qj & 0xFFu) + jx - 2 * cx, sy = (int)(qj >> 8) + jy - 2 * cy;
+        const int sx = (int)(qj & 0xFFu) + (int)(pj & 0xFFu) - 2 * cxb;
+        const int sy = (int)(qj >> 8) + (int)(pj >> 8) - 2 * cyb;
         if (j != aid && sx >= -1 && sx <= 1 && sy >= -1 && sy <= 1)
           dmask |= 1u << (uint32_t)((ACT_OF >> (4 * ((sx + 1) * 3 + sy + 1))) & 0xFu);
       }
     }
+    // the 3 x 3 around the agent is inside the window (S >= 4): its occupied cells are
+    // poss-plane bits (the centre is the agent itself, never a probe)
+    uint32_t nb9 = 0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int B = (H2 - 1 + r) * S + H2 - 1;
+      uint32_t v = possp[B >> 5] >> (B & 31);
+      if ((B & 31) > 29) v |= possp[(B >> 5) + 1] << (32 - (B & 31));
+      nb9 |= (v & 7u) << (3 * r);
+    }
     uint32_t goalp[4] = {0u, 0u, 0u, 0u};
     {
-      const int dx = gx - tr, dy = gy - tc;
+      const int dx = gxb - trb, dy = gyb - tcb;
       set_bit128(goalp, ((unsigned)dx < (unsigned)S && (unsigned)dy < (unsigned)S) ? (uint32_t)(dx * S + dy) : 127u);
     }
     // status (State.moveAgent), reward (:579-596), next valid actions (:639-667)
-    const bool on_old = gx == ox && gy == oy, on_new = gx == nx && gy == ny;
-    const int i9 = (dir_r(act) + 1) * 3 + dir_c(act) + 1;  // target cell in the 3 x 3 (when not moved, c = o)
+    const bool on_old = gA == ob, on_new = gA == tb;
+    const int i9 = (dir_r(act) + 1) * 3 + dir_c(act) + 1;  // target in the 3 x 3 (not moved: c = o)
     const bool wallT = ((w9 >> i9) & 1u) != 0;
     const int st_blocked = !inb ? -1 : (wallT ? -2 : -3);
     const int status = act == 0 ? (on_old ? 1 : 0) : (moved ? (on_new ? 1 : (on_old ? 2 : 0)) : st_blocked);
@@ -608,14 +630,14 @@ __global__ void __launch_bounds__(64) primal_seq_kernel(QGeo g, QArgs a) {
                                   : status == 1 ? GOAL_REWARD : status < 0 ? COLLISION_REWARD : ACTION_COST;
       if (a.reward) a.reward[oi] = rew;
       if (a.done) a.done[oi] = ngoal == N ? 1 : 0;
-      if (a.on_goal) a.on_goal[oi] = (cx == gx && cy == gy) ? 1 : 0;
+      if (a.on_goal) a.on_goal[oi] = gA == cb ? 1 : 0;
       if (a.valid) a.valid[oi] = status >= 0 ? 1 : 0;
       if (a.next_mask) {
         if constexpr (DIAG) ((uint16_t*)a.next_mask)[oi] = (uint16_t)mask;
         else a.next_mask[oi] = (uint8_t)mask;
       }
       if (a.vec) {  // :379-386, magnitude from the host libm pow LUT
-        const int dX = gx - cx, dY = gy - cy;
+        const int dX = gxb - cxb, dY = gyb - cyb;
         const double mag = a.pow_lut[dX * dX + dY * dY];
         double vx = (double)dX, vy = (double)dY;
         if (mag != 0.0) {
@@ -636,39 +658,41 @@ __global__ void __launch_bounds__(64) primal_seq_kernel(QGeo g, QArgs a) {
       put_plane<SS, SS, NSW>(str, goalp);
       put_plane<2 * SS, SS, NSW>(str, goalsp);
       put_plane<3 * SS, SS, NSW>(str, obsp);
-      uint32_t* dst = bstr + lane * 16;
+      // call k's 4 S^2 bits = 16-bit pieces CPC k .. CPC k + CPC - 1 of one contiguous
+      // string: the block's records are one run of bytes, piece c -> record bytes 16c ..
+      uint16_t* dst = bstr + CPC * lane;
 #pragma unroll
-      for (int i = 0; i < NSW; i += 4) {
-        uint4 v;
-        v.x = str[i];
-        v.y = i + 1 < NSW ? str[i + 1] : 0u;
-        v.z = i + 2 < NSW ? str[i + 2] : 0u;
-        v.w = i + 3 < NSW ? str[i + 3] : 0u;
-        *(uint4*)(dst + i) = v;
-      }
+      for (int i = 0; i < CPC; ++i) dst[i] = (uint16_t)(str[i >> 1] >> (16 * (i & 1)));
       wave_fence();
-      // the block's records are one contiguous run: 16-byte chunk c = bits 16q .. 16q + 15
-      // of call c / CPC's string (q = c % CPC), one bit per byte
-      const uint16_t* b16 = (const uint16_t*)bstr;
-      uint4* ob = (uint4*)(a.obs + (e0k + kb) * (4 * SS));
+      const uint32_t* b32 = (const uint32_t*)bstr;
+      uint4* obase = (uint4*)(a.obs + (e0k + kb) * (4 * SS));
       const int nch = nv * CPC;
-      for (int c = lane; c < nch; c += 64) {
-        const int k = c / CPC, q = c - k * CPC;
-        const uint32_t b = b16[k * 32 + q];
-        uint4 v;
-        v.x = ((b & 15u) * 0x00204081u) & 0x01010101u;
-        v.y = (((b >> 4) & 15u) * 0x00204081u) & 0x01010101u;
-        v.z = (((b >> 8) & 15u) * 0x00204081u) & 0x01010101u;
-        v.w = ((b >> 12) * 0x00204081u) & 0x01010101u;
-        ob[c] = v;
+      for (int i = lane; 2 * i < nch; i += 64) {
+        const uint32_t b = b32[i];
+        uint4 v0, v1;
+        v0.x = ((b & 15u) * 0x00204081u) & 0x01010101u;
+        v0.y = (((b >> 4) & 15u) * 0x00204081u) & 0x01010101u;
+        v0.z = (((b >> 8) & 15u) * 0x00204081u) & 0x01010101u;
+        v0.w = (((b >> 12) & 15u) * 0x00204081u) & 0x01010101u;
+        v1.x = (((b >> 16) & 15u) * 0x00204081u) & 0x01010101u;
+        v1.y = (((b >> 20) & 15u) * 0x00204081u) & 0x01010101u;
+        v1.z = (((b >> 24) & 15u) * 0x00204081u) & 0x01010101u;
+        v1.w = ((b >> 28) * 0x00204081u) & 0x01010101u;
+        if (MAPFX_QABL & 1) continue;
+        obase[2 * i] = v0;
+        if (2 * i + 1 < nch) obase[2 * i + 1] = v1;
       }
     }
     wave_fence();
   }
   if (agent) {
     const long long i = (long long)e * N + lane;
-    ((int2*)a.pos)[i] = make_int2((int)(vpos & 0xFFFFu), (int)(vpos >> 16));
-    if constexpr (DIAG) ((int2*)a.past)[i] = make_int2((int)(vpast & 0xFFFFu), (int)(vpast >> 16));
+    const uint32_t p = vpos - bias;
+    ((int2*)a.pos)[i] = make_int2((int)(p & 0xFFFFu), (int)(p >> 16));
+    if constexpr (DIAG) {
+      const uint32_t q = vpast - bias;
+      ((int2*)a.past)[i] = make_int2((int)(q & 0xFFFFu), (int)(q >> 16));
+    }
   }
 }
 
@@ -734,9 +758,9 @@ int layout_seq(QGeo& g) {
   g.off_gl = o;
   o += r16(4 * g.N);
   g.off_snap = o;
-  o += r16(64 * 2 * g.N);
+  o += r16(64 * 2 * g.N + 2);  // + the spare slot of the non-agent lanes
   g.off_psnap = o;
-  if (g.diag) o += r16(64 * 2 * g.N);
+  if (g.diag) o += r16(64 * 2 * g.N + 2);
   g.off_bstr = o;
   o += 64 * 64;
   return o;
@@ -863,8 +887,9 @@ void mapfx_primal_destroy(mapfx_primal_t* h) {
   delete h;
 }
 
-int mapfx_primal_act(mapfx_primal_t* h, const mapfx_primal_state* st, const int32_t* agent_ids,
-                     const int32_t* actions, int32_t K, const mapfx_primal_out* out, void* stream) {
+int mapfx_primal_act_timed(mapfx_primal_t* h, const mapfx_primal_state* st, const int32_t* agent_ids,
+                           const int32_t* actions, int32_t K, const mapfx_primal_out* out,
+                           void* start_event, void* stop_event, void* stream) {
   if (!h) return perr(MAPFX_EINVAL, "NULL handle");
   if (!st || !st->pos || !st->goal || !st->map_bits) return perr(MAPFX_EINVAL, "bad state");
   if (h->geo.diag && !st->past) return perr(MAPFX_EINVAL, "diagonal movement needs state.past");
@@ -893,12 +918,25 @@ int mapfx_primal_act(mapfx_primal_t* h, const mapfx_primal_state* st, const int3
   }
   const QGeo& g = h->geo;
   if (g.seq && ((uintptr_t)a.obs & 15u) == 0) {  // (16-byte record runs)
-    hipLaunchKernelGGL(pick_seq(g), dim3(g.E), dim3(64), g.lds_seq, (hipStream_t)stream, g, a);
+    if (start_event || stop_event)
+      hipExtLaunchKernelGGL(pick_seq(g), dim3(g.E), dim3(64), g.lds_seq, (hipStream_t)stream,
+                            (hipEvent_t)start_event, (hipEvent_t)stop_event, 0, g, a);
+    else
+      hipLaunchKernelGGL(pick_seq(g), dim3(g.E), dim3(64), g.lds_seq, (hipStream_t)stream, g, a);
     return check_hip(hipGetLastError(), "primal_seq_kernel launch");
   }
   const int wpw = 64 >> g.lw_shift;
-  hipLaunchKernelGGL(pick_primal(g), dim3((g.E + wpw - 1) / wpw), dim3(64), h->lds, (hipStream_t)stream, g, a);
+  if (start_event || stop_event)
+    hipExtLaunchKernelGGL(pick_primal(g), dim3((g.E + wpw - 1) / wpw), dim3(64), h->lds, (hipStream_t)stream,
+                          (hipEvent_t)start_event, (hipEvent_t)stop_event, 0, g, a);
+  else
+    hipLaunchKernelGGL(pick_primal(g), dim3((g.E + wpw - 1) / wpw), dim3(64), h->lds, (hipStream_t)stream, g, a);
   return check_hip(hipGetLastError(), "primal_act_kernel launch");
+}
+
+int mapfx_primal_act(mapfx_primal_t* h, const mapfx_primal_state* st, const int32_t* agent_ids,
+                     const int32_t* actions, int32_t K, const mapfx_primal_out* out, void* stream) {
+  return mapfx_primal_act_timed(h, st, agent_ids, actions, K, out, nullptr, nullptr, stream);
 }
 
 }  // extern "C"

@@ -94,7 +94,7 @@ EXPORTS = ("mapfx_abi_version", "mapfx_last_error", "mapfx_map_stride", "mapfx_o
            "mapfx_partial_goal_dist_elem_size",
            "mapfx_partial_goal_dist", "mapfx_partial_reset", "mapfx_partial_step",
            "mapfx_partial_observe", "mapfx_primal_create", "mapfx_primal_destroy",
-           "mapfx_primal_act", "mapfx_runner_begin", "mapfx_runner_actions", "mapfx_runner_post",
+           "mapfx_primal_act", "mapfx_primal_act_timed", "mapfx_runner_begin", "mapfx_runner_actions", "mapfx_runner_post",
            "mapfx_runner_step", "mapfx_host_ring_alloc", "mapfx_host_ring_free")
 
 
@@ -152,6 +152,7 @@ def _load():
         "mapfx_primal_create": (c_i32, [P(QCfg), P(c_vp)]),
         "mapfx_primal_destroy": (None, [c_vp]),
         "mapfx_primal_act": (c_i32, [c_vp, P(QState), c_vp, c_vp, c_i32, P(QOut), c_vp]),
+        "mapfx_primal_act_timed": (c_i32, [c_vp, P(QState), c_vp, c_vp, c_i32, P(QOut), c_vp, c_vp, c_vp]),
         "mapfx_runner_begin": (c_i32, [P(RState), P(POut), P(ERows), c_vp]),
         "mapfx_runner_actions": (c_i32, [P(RState), c_vp, c_i32, c_i64, c_i32, P(ERows), c_vp]),
         "mapfx_runner_post": (c_i32, [P(RState), c_vp, P(POut), c_i32, c_vp, P(ERows), c_vp]),

@@ -109,10 +109,12 @@ class PrimalBatch:
         self._out = _abi.QOut(err=ptr(self.err), **{k: ptr(self.out[k]) for k in _OUT_KEYS})
         self._K = K
 
-    def act(self, agent_ids, actions):
+    def act(self, agent_ids, actions, events=None):
         """K calls of `_step((agent_id, action))` per world, in order.
         agent_ids (1-based) / actions: [E, K] ints.  Returns the output dict,
-        each entry [E, K, ...] (buffers reused by the next call with the same K)."""
+        each entry [E, K, ...] (buffers reused by the next call with the same K).
+        events: optional (start, stop) torch.cuda.Event pair recorded at the
+        kernel's own begin / end (mapfx_primal_act_timed)."""
         ids = torch.as_tensor(agent_ids, device=self.device).to(torch.int32).contiguous()
         acts = torch.as_tensor(actions, device=self.device).to(torch.int32).contiguous()
         if ids.ndim != 2 or ids.shape[0] != self.E or acts.shape != ids.shape:
@@ -121,10 +123,17 @@ class PrimalBatch:
         if K != self._K:
             self._alloc(K)
         with torch.cuda.device(self.device):
-            check(lib.mapfx_primal_act(self._h, ctypes.byref(self._state), ptr(ids), ptr(acts), K,
-                                       ctypes.byref(self._out),
-                                       torch.cuda.current_stream().cuda_stream),
-                  "mapfx_primal_act")
+            if events is None:
+                check(lib.mapfx_primal_act(self._h, ctypes.byref(self._state), ptr(ids), ptr(acts), K,
+                                           ctypes.byref(self._out),
+                                           torch.cuda.current_stream().cuda_stream),
+                      "mapfx_primal_act")
+            else:
+                check(lib.mapfx_primal_act_timed(self._h, ctypes.byref(self._state), ptr(ids), ptr(acts),
+                                                 K, ctypes.byref(self._out), events[0].cuda_event,
+                                                 events[1].cuda_event,
+                                                 torch.cuda.current_stream().cuda_stream),
+                      "mapfx_primal_act_timed")
         return self.out
 
     def check_err(self):

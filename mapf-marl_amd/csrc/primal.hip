@@ -448,25 +448,32 @@ __global__ void __launch_bounds__(64) primal_seq_kernel(QGeo g, QArgs a) {
   const int lane = threadIdx.x, e = blockIdx.x;
   const int N = g.N, H = g.H, W = g.W, P = g.P;
   uint64_t* rowm = (uint64_t*)lds;                   // [H + 2P] padded wall rows
-  uint32_t* gl = (uint32_t*)(lds + g.off_gl);        // [N] biased goal (row + P) | (col + P) << 16
-  uint16_t* snap = (uint16_t*)(lds + g.off_snap);    // [64][N] biased row | col << 8 after call k
-  uint16_t* psnap = (uint16_t*)(lds + g.off_psnap);  // DIAG: agents_past after call k
+  uint32_t* gl = (uint32_t*)(lds + g.off_gl);        // [N] biased goal cell
+  uint16_t* snap = (uint16_t*)(lds + g.off_snap);    // [65][N] cells before call 0, after calls 0..63
+  uint16_t* psnap = (uint16_t*)(lds + g.off_psnap);  // DIAG: agents_past, same rows
   uint16_t* bstr = (uint16_t*)(lds + g.off_bstr);    // the block's bit strings, call k at CPC * k
   const int2* goal2 = (const int2*)a.goal + (long long)e * N;  // wave-uniform reads: SGPRs
 
-  // ---- state: lane j = agent j at the BIASED cell (row + P) | (col + P) << 16, which is
-  //      also its padded-map coordinate; other lanes hold a value no cell has ----
+  // ---- state: lane j = agent j at its BIASED cell (row + P) | (col + P) << 8 (rows and
+  //      columns of the padded map, < 64: the cell is its own u16 snapshot value and a
+  //      move is one packed add); other lanes hold a value no cell has ----
   const bool agent = lane < N;
-  const uint32_t bias = (uint32_t)P | ((uint32_t)P << 16);
+  const uint32_t bias = (uint32_t)P | ((uint32_t)P << 8);
+  // block 0's calls are loaded first: their latency overlaps the set-up loads
+  int id0 = 0, ac0 = 0;
+  if (lane < min(64, a.K)) {
+    id0 = a.ids[(long long)e * a.K + lane];
+    ac0 = a.acts[(long long)e * a.K + lane];
+  }
   uint32_t vpos = 0xFFFFFFFFu, vpast = 0u;
   if (agent) {
     const long long i = (long long)e * N + lane;
     const int2 p = ((const int2*)a.pos)[i], q = goal2[lane];
-    vpos = ((uint32_t)p.x | ((uint32_t)p.y << 16)) + bias;
-    gl[lane] = ((uint32_t)q.x | ((uint32_t)q.y << 16)) + bias;
+    vpos = ((uint32_t)p.x | ((uint32_t)p.y << 8)) + bias;
+    gl[lane] = ((uint32_t)q.x | ((uint32_t)q.y << 8)) + bias;
     if constexpr (DIAG) {
       const int2 pp = ((const int2*)a.past)[i];
-      vpast = ((uint32_t)pp.x | ((uint32_t)pp.y << 16)) + bias;
+      vpast = ((uint32_t)pp.x | ((uint32_t)pp.y << 8)) + bias;
     }
   }
   uint32_t vsum = vpos + vpast;  // DIAG: past + present, the midpoint test's sum (sentinel off-agent)
@@ -493,24 +500,26 @@ __global__ void __launch_bounds__(64) primal_seq_kernel(QGeo g, QArgs a) {
   for (int kb = 0; kb < kstop; kb += 64) {
     const int nb = min(64, a.K - kb);
     // call kb + lane: agent index, action, and the move as one packed add (cells biased,
-    // so a row step never borrows from the column half); the first bad call ends the
+    // so a row step never borrows from the column byte); the first bad call ends the
     // world's calls (the reference asserts, :556-558)
-    bool okc = false;
-    int id = 0, ac = 0;
-    if (lane < nb) {
+    int id = id0, ac = ac0;
+    if (kb > 0 && lane < nb) {
       id = a.ids[e0k + kb + lane];
       ac = a.acts[e0k + kb + lane];
-      okc = (unsigned)(id - 1) < (unsigned)N && (unsigned)ac < (unsigned)g.nact;
     }
+    const bool okc = lane < nb && (unsigned)(id - 1) < (unsigned)N && (unsigned)ac < (unsigned)g.nact;
     const uint64_t badm = __ballot(lane < nb && !okc);
     const int nv = badm ? (int)__ffsll((unsigned long long)badm) - 1 : nb;
     const int vaid = okc ? id - 1 : 0, vact = okc ? ac : 0;
-    const uint32_t vdel = okc ? (uint32_t)(dir_r(ac) + dir_c(ac) * 65536) : 0u;
+    const uint32_t vdel = okc ? (uint32_t)(dir_r(ac) + dir_c(ac) * 256) : 0u;
     // ================= phase A: State.moveAgent, call after call =================
-    uint32_t vlog = bias;  // (biased (0, 0) for lanes without a call: in-range reads below)
-    // snapshot slots: agent lanes write [kk][lane], the others one spare slot past the rows
-    uint32_t saddr = agent ? 2u * (uint32_t)lane : 2u * 64u * (uint32_t)N;
+    // snapshot rows: row 0 = the cells before call kb, row kk + 1 = after call kb + kk;
+    // agent lanes write slot [row][lane], the others one spare slot past the rows
+    uint32_t saddr = agent ? 2u * (uint32_t)lane : 2u * 65u * (uint32_t)N;
     const uint32_t sinc = agent ? 2u * (uint32_t)N : 0u;
+    *(uint16_t*)((unsigned char*)snap + saddr) = (uint16_t)vpos;
+    if constexpr (DIAG) *(uint16_t*)((unsigned char*)psnap + saddr) = (uint16_t)vpast;
+    saddr += sinc;
     for (int kk = 0; kk < nv; ++kk) {
       if (MAPFX_QABL & 4) {
         *(uint16_t*)((unsigned char*)snap + saddr) = (uint16_t)vpos;
@@ -520,23 +529,19 @@ __global__ void __launch_bounds__(64) primal_seq_kernel(QGeo g, QArgs a) {
       const int aid = __builtin_amdgcn_readlane(vaid, kk);
       const uint32_t d = readlane_u32(vdel, kk);
       const uint32_t o = readlane_u32(vpos, aid), t = o + d;
-      const int rs = (int)(t & 0xFFFFu);  // padded row of the target (outside = wall)
+      const int rs = (int)(t & 0xFFu);  // padded row of the target (outside = wall)
       const uint64_t wr = ((uint64_t)readlane_u32(vrow_hi, rs) << 32) | readlane_u32(vrow_lo, rs);
       // wall / outside, or an agent on the target (a stay hits itself)
-      uint64_t blk = ((wr >> (t >> 16)) & 1ull) | __ballot(vpos == t);
-      if constexpr (DIAG) blk |= __ballot(vsum == o + t && lane != aid);
-      const bool moved = blk == 0;
-      if (lane == aid) {
-        if constexpr (DIAG) {
-          if (d == 0u || moved) vpast = o;  // agents_past (:110-112, :129-131)
-        }
-        if (moved) vpos = t;
-      }
+      uint64_t blk = ((wr >> (t >> 8)) & 1ull) | __ballot(vpos == t);
+      if constexpr (DIAG) blk |= __ballot(vsum == o + t && vpos != o);  // (vpos == o: agent aid)
+      uint32_t tm = blk == 0 ? t : o;  // agent aid's cell after the call
+      asm volatile("" : "+s"(tm));      // (uniform, computed before the select: no exec branch)
+      const bool me = vpos == o;        // (cells are distinct: only lane aid)
+      if constexpr (DIAG) vpast = (me && (d == 0u || tm != o)) ? o : vpast;  // agents_past (:110-112, :129-131)
+      vpos = me ? tm : vpos;
       if constexpr (DIAG) vsum = vpos + vpast;
-      if (lane == kk) vlog = o | (moved ? 0x80000000u : 0u);
-      const uint16_t sv = (uint16_t)((vpos & 0xFFu) | ((vpos >> 8) & 0xFF00u));
-      *(uint16_t*)((unsigned char*)snap + saddr) = sv;
-      if constexpr (DIAG) *(uint16_t*)((unsigned char*)psnap + saddr) = (uint16_t)((vpast & 0xFFu) | ((vpast >> 8) & 0xFF00u));
+      *(uint16_t*)((unsigned char*)snap + saddr) = (uint16_t)vpos;
+      if constexpr (DIAG) *(uint16_t*)((unsigned char*)psnap + saddr) = (uint16_t)vpast;
       saddr += sinc;
     }
     if (nv < nb) {
@@ -548,13 +553,16 @@ __global__ void __launch_bounds__(64) primal_seq_kernel(QGeo g, QArgs a) {
     if (MAPFX_QABL & 2) continue;
     const bool cv = lane < nv;
     const int aid = vaid, act = vact;
-    const uint32_t ob = vlog & 0x7FFFFFFFu, tb = ob + vdel;
-    const bool moved = (vlog >> 31) != 0;
-    const uint32_t cb = moved ? tb : ob;
-    const int cxb = (int)(cb & 0xFFFFu), cyb = (int)(cb >> 16);
-    const bool inb = (unsigned)((int)(tb & 0xFFFFu) - P) < (unsigned)H && (unsigned)((int)(tb >> 16) - P) < (unsigned)W;
+    // call k's cell before / after it: snapshot rows k and k + 1 (lanes without a call: the
+    // biased (0, 0), so the reads below stay inside the padded map)
+    const uint32_t ob = cv ? (uint32_t)snap[lane * N + aid] : bias;
+    const uint32_t cb = cv ? (uint32_t)snap[(lane + 1) * N + aid] : bias;
+    const uint32_t tb = ob + vdel;
+    const bool moved = cb != ob;
+    const int cxb = (int)(cb & 0xFFu), cyb = (int)(cb >> 8);
+    const bool inb = (unsigned)((int)(tb & 0xFFu) - P) < (unsigned)H && (unsigned)((int)(tb >> 8) - P) < (unsigned)W;
     const uint32_t gA = gl[aid];
-    const int gxb = (int)(gA & 0xFFFFu), gyb = (int)(gA >> 16);
+    const int gxb = (int)(gA & 0xFFu), gyb = (int)(gA >> 8);
     const int trb = cxb - H2, tcb = cyb - H2;  // window origin in padded coordinates
     // obstacle plane (:356-362, outside = 1) and the walls of the 3 x 3 around the agent
     uint32_t obsp[4] = {0u, 0u, 0u, 0u};
@@ -573,8 +581,8 @@ __global__ void __launch_bounds__(64) primal_seq_kernel(QGeo g, QArgs a) {
     uint32_t possp[4] = {0u, 0u, 0u, 0u}, goalsp[4] = {0u, 0u, 0u, 0u};
     uint32_t dmask = 0;
     int ngoal = 0;
-    const uint16_t* sk = snap + lane * N;
-    const uint16_t* pk = psnap + lane * N;
+    const uint16_t* sk = snap + (lane + 1) * N;
+    const uint16_t* pk = psnap + (lane + 1) * N;
     for (int j = 0; j < N; ++j) {
       const int2 gj = goal2[j];
       const int gjxb = gj.x + P, gjyb = gj.y + P;
@@ -688,10 +696,10 @@ __global__ void __launch_bounds__(64) primal_seq_kernel(QGeo g, QArgs a) {
   if (agent) {
     const long long i = (long long)e * N + lane;
     const uint32_t p = vpos - bias;
-    ((int2*)a.pos)[i] = make_int2((int)(p & 0xFFFFu), (int)(p >> 16));
+    ((int2*)a.pos)[i] = make_int2((int)(p & 0xFFu), (int)(p >> 8));
     if constexpr (DIAG) {
       const uint32_t q = vpast - bias;
-      ((int2*)a.past)[i] = make_int2((int)(q & 0xFFFFu), (int)(q >> 16));
+      ((int2*)a.past)[i] = make_int2((int)(q & 0xFFu), (int)(q >> 8));
     }
   }
 }
@@ -758,9 +766,9 @@ int layout_seq(QGeo& g) {
   g.off_gl = o;
   o += r16(4 * g.N);
   g.off_snap = o;
-  o += r16(64 * 2 * g.N + 2);  // + the spare slot of the non-agent lanes
+  o += r16(65 * 2 * g.N + 2);  // 65 rows + the spare slot of the non-agent lanes
   g.off_psnap = o;
-  if (g.diag) o += r16(64 * 2 * g.N + 2);
+  if (g.diag) o += r16(65 * 2 * g.N + 2);
   g.off_bstr = o;
   o += 64 * 64;
   return o;

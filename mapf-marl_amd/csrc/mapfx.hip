@@ -33,6 +33,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <utility>
 #include <new>
 #include <string>
@@ -92,6 +93,10 @@ struct Geo {
   int off_map, off_bits, off_oldc, off_newc, off_rc, off_goal, off_rew, off_flag;
   int map_env_bytes, bits_env_bytes, stage_env_bytes;
   int gen_lds;             // dynamic LDS of a generic-kernel block
+  // deferred reward fold of the generic rollout (one env per block): per-agent reward
+  // CODES of the last fold_R steps in an LDS ring at off_rew (fold_R = 0: per-step
+  // fold), code_pitch bytes per step, and the fp64 rewards of the codes < 32 at off_ctab
+  int fold_R, code_pitch, off_ctab;
   uint64_t m_N, m_w, m_ww, m_wlen;  // fastdiv magics for the block-cooperative window writer
   int window, wlen;        // marl_partial window w, 2*w*w
   int psize;               // PRIMAL observation size s
@@ -242,6 +247,15 @@ __device__ __forceinline__ __attribute__((unused)) uint32_t lds_addr(const void*
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
+#ifndef MAPFX_FOLD_R
+#define MAPFX_FOLD_R 8  // deferred-fold ring depth of the generic rollout (power of two; 0 = off)
+#endif
+#ifndef MAPFX_OCC_U
+#define MAPFX_OCC_U 0   // rows in flight per thread in write_occ16_rows (0: by window size)
+#endif
+#ifndef MAPFX_W0_WRITES
+#define MAPFX_W0_WRITES 1  // wave 0 writes window records on the steps without a fold
+#endif
 #ifndef MAPFX_GABL
 #define MAPFX_GABL 0  // diagnostic builds only: generic-kernel parts skipped for timing
 #endif
@@ -354,36 +368,58 @@ __device__ void write_occ16_rows(const Geo& g, const unsigned char* lds, const i
                                  unsigned char* dst, int nseg, int tid, int nt) {
   constexpr int NP = (W + 1) / 2;  // cell pairs per row (the last one half used)
   constexpr int h = W / 2;
+  constexpr int U = MAPFX_OCC_U > 0 ? MAPFX_OCC_U : (W <= 5 ? 4 : 2);  // rows in flight per thread
   typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
   const int pitch = g.pitch;
+  const bool one_env = g.EPB == 1;
   const uint32_t lbase = lds_addr(lds + g.off_map);
-  for (int sg = tid; sg < nseg; sg += nt) {
-    const int q = fastdiv(sg, g.m_w);
-    const int y = sg - q * W;
-    const int slot = fastdiv(q, g.m_N);
-    const int e0 = newc_blk[q] + (y - h) * pitch - h;          // first cell of the row
-    const uint32_t A = lbase + (uint32_t)(slot * g.map_env_bytes) + 2u * (uint32_t)e0;
-    lds_cu32* src = (lds_cu32*)(uintptr_t)(A & ~3u);
-    uint32_t Wd[NP + 1];
+  const bool dalign = (((uintptr_t)dst) & 2u) == 0;
+  for (int sg0 = tid; sg0 < nseg; sg0 += U * nt) {
+    int q[U], y[U];
+    bool ok[U];
 #pragma unroll
-    for (int j = 0; j <= NP; ++j) Wd[j] = src[j];
-    const uint32_t sh = A & 2u;
-    uint32_t P[NP];
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const uint32_t c = __builtin_amdgcn_alignbyte(Wd[j + 1], Wd[j], sh);
-      P[j] = (((c & 0x7FFF7FFFu) | 0x80008000u) - ((c >> 15) & 0x00010001u)) ^ 0x80008000u;
+    for (int u = 0; u < U; ++u) {
+      const int sg = sg0 + u * nt;
+      ok[u] = sg < nseg;
+      const int sv = ok[u] ? sg : sg0;
+      q[u] = fastdiv(sv, g.m_w);
+      y[u] = sv - q[u] * W;
     }
-    const uint32_t O = 2u * (uint32_t)(q * (W * W) + y * W);
-    if ((((uintptr_t)dst + O) & 2u) == 0) {  // parity of the absolute address (dst may be 2 mod 4)
+    int nq[U];
 #pragma unroll
-      for (int j = 0; j + 1 < NP; ++j) *(uint32_t*)(dst + O + 4 * j) = P[j];
-      *(uint16_t*)(dst + O + 4 * (NP - 1)) = (uint16_t)P[NP - 1];
-    } else {
-      *(uint16_t*)(dst + O) = (uint16_t)P[0];
+    for (int u = 0; u < U; ++u) nq[u] = newc_blk[q[u]];
+    uint32_t Wd[U][NP + 1], sh[U];
 #pragma unroll
-      for (int j = 0; j + 1 < NP; ++j)
-        *(uint32_t*)(dst + O + 2 + 4 * j) = __builtin_amdgcn_alignbyte(P[j + 1], P[j], 2);
+    for (int u = 0; u < U; ++u) {
+      const int slot = one_env ? 0 : fastdiv(q[u], g.m_N);
+      const int e0 = nq[u] + (y[u] - h) * pitch - h;  // first cell of the row
+      const uint32_t A = lbase + (uint32_t)(slot * g.map_env_bytes) + 2u * (uint32_t)e0;
+      lds_cu32* src = (lds_cu32*)(uintptr_t)(A & ~3u);
+#pragma unroll
+      for (int j = 0; j <= NP; ++j) Wd[u][j] = src[j];
+      sh[u] = A & 2u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      uint32_t P[NP];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        const uint32_t c = __builtin_amdgcn_alignbyte(Wd[u][j + 1], Wd[u][j], sh[u]);
+        P[j] = (((c & 0x7FFF7FFFu) | 0x80008000u) - ((c >> 15) & 0x00010001u)) ^ 0x80008000u;
+      }
+      const uint32_t O = 2u * (uint32_t)(q[u] * (W * W) + y[u] * W);
+      unsigned char* d = dst + O;
+      if (dalign == ((O & 2u) == 0)) {  // parity of the absolute address (dst may be 2 mod 4)
+#pragma unroll
+        for (int j = 0; j + 1 < NP; ++j) *(uint32_t*)(d + 4 * j) = P[j];
+        *(uint16_t*)(d + 4 * (NP - 1)) = (uint16_t)P[NP - 1];
+      } else {
+        *(uint16_t*)d = (uint16_t)P[0];
+#pragma unroll
+        for (int j = 0; j + 1 < NP; ++j)
+          *(uint32_t*)(d + 2 + 4 * j) = __builtin_amdgcn_alignbyte(P[j + 1], P[j], 2);
+      }
     }
   }
 }
@@ -395,6 +431,20 @@ __device__ void write_occ16_rows(const Geo& g, const unsigned char* lds, const i
 // VGPRs, i.e. 4 blocks of 256 threads per CU.
 // ---------------------------------------------------------------------------
 constexpr int FEAT_PRIM = 1, FEAT_FULL = 2;
+
+// The fp64 reward of one agent from its reward code (deferred fold): bit 0 counted
+// (not done before the step), bit 1 env collision, bit 2 node collision, bits 3.. the
+// edge-collision count -- the op order of the per-step computation below (:94-130).
+__device__ inline double code_reward(const Geo& g, uint32_t c) {
+  double rr = 0.0;
+  if (c & 1u) {
+    if (c & 2u) rr = rr + g.collide_rew;
+    rr = rr + g.step_rew;
+  }
+  rr = rr + g.collide_rew * (double)((c >> 2) & 1u);
+  rr = rr + g.collide_rew * (double)(c >> 3);
+  return rr;
+}
 template <typename CellT, int APL, bool ROLL, int FEAT>
 __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   using CT = CellTraits<CellT>;
@@ -416,6 +466,14 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   int* gls = (int*)(lds + g.off_goal) + slot * N;
   double* rew = (double*)(lds + g.off_rew) + slot * N;  // aliases bitsL (used after the build)
   int* flag = (int*)(lds + g.off_flag) + slot * 8;  // [parity*4 + {alldone, bad}]
+  // Deferred fold (rollouts, one env per block): every step stores a u16 reward CODE
+  // per agent in a ring of FR rows (aliasing rew / the bitmap); every FR-th step (and
+  // the last) lanes 0..FR-1 of wave 0 fold one row each -- the same agent-order chain
+  // of fp64 adds per step, FR steps' chains side by side -- so the other steps carry no
+  // fold and wave 0 writes window records with the others.
+  const int FR = (ROLL && a.do_step) ? g.fold_R : 0;
+  uint16_t* codes = (uint16_t*)(lds + g.off_rew);
+  double* ctab = (double*)(lds + g.off_ctab);  // code_reward of the codes < 32
 
   // ---- per-lane agent state (registers) ----
   int r[APL], c[APL], gr[APL], gc[APL], st[APL];
@@ -448,6 +506,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     for (int w = lane; w < g.bits_words; w += g.L) bitsL[w] = src[w];
   }
   for (int i = lane; i < 8; i += g.L) flag[i] = (i & 3) == 0 ? 1 : 0;  // alldone = 1, bad = 0
+  if (FR && tid < 32) ctab[tid] = code_reward(g, (uint32_t)tid);
   __syncthreads();
   fill_map<CellT>(g, map32, bitsL, lane);
   __syncthreads();
@@ -555,19 +614,40 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
 #pragma unroll
     for (int k = 0; k < APL; ++k) edgek[k] = 0;
     if (g.L >= 64 && a.do_step && !skip && !(MAPFX_GABL & 8)) {
+      // the env's (old, new) cells, 64 agents per chunk, read once by a wave that
+      // has such an i; each i's count is then one ballot popcount per chunk
+      constexpr int NCH = APL * 4;  // N <= APL * 256
       const int l64 = tid & 63;
+      const int nch = (N + 63) >> 6;
+      uint64_t mk[APL];
+      bool any = false;
 #pragma unroll
       for (int k = 0; k < APL; ++k) {
-        uint64_t m = __ballot(has[k] && moved[k] && pre[k] > 0);
-        while (m) {
-          const int src = __ffsll((unsigned long long)m) - 1;
-          m &= m - 1;
-          const int tn = __shfl(nc[k], src), to = __shfl(oc[k], src);
-          int cnt = 0;
-          for (int j = l64; j < N; j += 64) cnt += (oldc[j] == tn) & (newc[j] == to);
+        mk[k] = __ballot(has[k] && moved[k] && pre[k] > 0);
+        any |= mk[k] != 0;
+      }
+      if (any) {
+        int jo[NCH], jn[NCH];
 #pragma unroll
-          for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d);
-          if (l64 == src) edgek[k] = cnt;
+        for (int q = 0; q < NCH; ++q) {
+          const int j = q * 64 + l64;
+          const bool ok = q < nch && j < N;
+          jo[q] = ok ? oldc[j] : -1;
+          jn[q] = ok ? newc[j] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < APL; ++k) {
+          uint64_t m = mk[k];
+          while (m) {
+            const int src = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            const int tn = __shfl(nc[k], src), to = __shfl(oc[k], src);
+            int cnt = 0;
+#pragma unroll
+            for (int q = 0; q < NCH; ++q)
+              if (q < nch) cnt += __popcll(__ballot((jo[q] == tn) & (jn[q] == to)));
+            if (l64 == src) edgek[k] = cnt;
+          }
         }
       }
     }
@@ -583,17 +663,26 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
           for (int j = 0; j < N; ++j)
             edge += (oldc[j] == nc[k]) & (newc[j] == oc[k]);
         }
-        double rr = 0.0;  // :94-130, exact fp64 op order
-        if (!dn[k]) {
-          if (envc[k]) rr = rr + g.collide_rew;
-          rr = rr + g.step_rew;
-          ++st[k];
+        if (FR) {  // the reward's code (code_reward); folded every FR steps
+          codes[(s & (FR - 1)) * (g.code_pitch >> 1) + ag] =
+              (uint16_t)((dn[k] ? 0u : 1u) | (envc[k] ? 2u : 0u) | ((uint32_t)node << 2) |
+                         ((uint32_t)edge << 3));
+          if (!dn[k]) ++st[k];
+        } else {
+          double rr = 0.0;  // :94-130, exact fp64 op order
+          if (!dn[k]) {
+            if (envc[k]) rr = rr + g.collide_rew;
+            rr = rr + g.step_rew;
+            ++st[k];
+          }
+          rr = rr + g.collide_rew * (double)node;
+          rr = rr + g.collide_rew * (double)edge;
+          rew[ag] = rr;
         }
-        rr = rr + g.collide_rew * (double)node;
-        rr = rr + g.collide_rew * (double)edge;
-        rew[ag] = rr;
         if (r[k] == gr[k] && c[k] == gc[k]) dn[k] = true;  // :112-114
         if (tcur >= g.limit) dn[k] = true;                   // :116-117
+      } else if (FR) {
+        codes[(s & (FR - 1)) * (g.code_pitch >> 1) + ag] = 0;  // code_reward(0) = 0.0
       } else if (a.do_step) {
         rew[ag] = 0.0;
       }
@@ -624,7 +713,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       if (a.do_step) {
         if (fl[1] && a.err) atomicCAS(a.err, 0, env + 1);
         double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
-        if (!(MAPFX_GABL & 1)) {
+        if (!(MAPFX_GABL & 1) && !FR) {
           // the adds are one dependent chain; a ring of 8 LDS reads stays in flight
           // ahead of it (the read of reward j + 8 is issued when reward j is added)
           int j = 0;
@@ -648,8 +737,10 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
           }
           for (; j < N; ++j) R = R + rew[j];
         }
-        if (a.reward) a.reward[slotE + env] = R;
-        if (a.reward_f32) a.reward_f32[slotE + env] = (float)R;
+        if (!FR) {
+          if (a.reward) a.reward[slotE + env] = R;
+          if (a.reward_f32) a.reward_f32[slotE + env] = (float)R;
+        }
       }
       if (a.term) a.term[slotE + env] = alldone ? 1 : 0;
       if (a.traj_t) a.traj_t[slotE + env] = tcur;
@@ -657,14 +748,41 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       nf[0] = 1;
       nf[1] = 0;
     };
+    // ---- deferred fold: lane i < FR of wave 0 folds the code row of step s0 + i ----
+    const bool fstep = FR && (((s & (FR - 1)) == FR - 1) || s + 1 == T);
+    auto fold_ring = [&]() {
+      const int s0 = s & ~(FR - 1);
+      if (!env_ok || tid > s - s0 || (MAPFX_GABL & 1)) return;
+      const uint16_t* cs = codes + tid * (g.code_pitch >> 1);
+      auto val = [&](uint32_t c) { return c < 32u ? ctab[c] : code_reward(g, c); };
+      double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
+      int j = 0;
+      for (; j + 8 <= N; j += 8) {
+        const uint4 v = *(const uint4*)(cs + j);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          R = R + val(w[i] & 0xFFFFu);
+          R = R + val(w[i] >> 16);
+        }
+      }
+      for (; j < N; ++j) R = R + val(cs[j]);
+      const long long ri = (long long)(s0 + tid) * Elong + env;
+      if (a.reward) a.reward[ri] = R;
+      if (a.reward_f32) a.reward_f32[ri] = (float)R;
+    };
     // One env per block over four waves (N > 128): wave 0 runs the tail (the fold is
-    // one dependent chain of N adds) while waves 1-3 write the window records.
+    // one dependent chain of N adds) while waves 1-3 write the window records; with
+    // the deferred fold, wave 0 writes records too except on the fold steps.
     const bool ovl = g.L == 256 && (a.obs_window || a.obs_window_occ);
     if (ovl) {
-      lds_barrier();  // B2b: rew[] and the alldone flag complete
-      if (tid < 64) lane0_tail(fl[0] != 0);
+      lds_barrier();  // B2b: rew[] / codes and the alldone flag complete
+      if (tid < 64) {
+        lane0_tail(fl[0] != 0);
+        if (fstep) fold_ring();
+      }
     }
-    const int wt0 = ovl ? 64 : 0;  // first writer thread
+    const int wt0 = (ovl && (!FR || fstep || !MAPFX_W0_WRITES)) ? 64 : 0;  // first writer thread
     if ((a.obs_window || a.obs_window_occ) && !(MAPFX_GABL & 2) && tid >= wt0) {  // :323-342
       const int wtid = tid - wt0, wnt = g.BT - wt0;
       const int nenv = min(g.EPB, g.E - env0);
@@ -771,7 +889,10 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     lds_barrier();  // B3: rew[] and flags complete
     // ================= P3: fold, term, staging copy-out, autoreset =================
     const bool alldone = fl[0] != 0;
-    if (!ovl) lane0_tail(alldone);
+    if (!ovl) {
+      lane0_tail(alldone);
+      if (fstep && tid < 64) fold_ring();
+    }
     // optional autoreset of envs whose agents are all done
 #pragma unroll
     for (int k = 0; k < APL; ++k) {
@@ -791,7 +912,10 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       }
     }
     if (a.autoreset && alldone && a.do_step) tcur = 0;
-    if (ROLL && s + 1 < T) lds_barrier();  // B4: map reuse by the next step
+    // B4: the autoreset's map atomics, and (without the overlap) the tail's reset of the
+    // next step's flags, before the next step; with the overlap and no autoreset every
+    // hand-off of this step is already ordered by B3
+    if (ROLL && s + 1 < T && (a.autoreset || !ovl)) lds_barrier();
   }
 
   // ---- write back the env state ----
@@ -2734,10 +2858,27 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     off += round_up(EPB * N * 4, 16);
   }
   g.off_bits = g.off_rew = off;  // the bitmap is dead once the map is built
-  off += std::max(EPB * g.bits_env_bytes, round_up(EPB * N * 8, 16));
+  const int rew_bytes = std::max(EPB * g.bits_env_bytes, round_up(EPB * N * 8, 16));
+  off += rew_bytes;
   g.off_flag = off;
   off += round_up(EPB * 8 * 4, 16);
   g.gen_lds = off;
+  // Deferred fold (rollouts with one env per block): the ring of FOLD_R code rows
+  // replaces the fp64 reward row, and is kept only when the block count per CU stays.
+  g.fold_R = 0;
+  g.code_pitch = round_up(2 * N, 16) + 16;  // +16 B: the fold lanes' rows start on other banks
+  g.off_ctab = -1;
+  if (MAPFX_FOLD_R > 0 && EPB == 1 && L >= 64 && std::isfinite(c.step_reward) && std::isfinite(c.collide_reward)) {
+    constexpr int FOLD_R = MAPFX_FOLD_R;
+    const int ring = std::max(rew_bytes, FOLD_R * g.code_pitch);
+    const int lds_f = g.gen_lds - rew_bytes + ring + 32 * 8;
+    if (LDS_MAX / lds_f >= LDS_MAX / g.gen_lds) {
+      g.fold_R = FOLD_R;
+      g.off_flag = g.off_rew + ring;
+      g.off_ctab = g.off_flag + round_up(EPB * 8 * 4, 16);
+      g.gen_lds = lds_f;  // step launches share the layout (the ring is unused there)
+    }
+  }
 
   // wave-local fast path layout (one wavefront = EPW envs)
   g.wave_ok = 0;

@@ -799,6 +799,8 @@ def test_stacked_swap_edge_count_exact(mapfx_mod, N):
     b2.reset()
     traj = b2.rollout(1, actions=torch.from_numpy(a[None]).cuda())
     assert np.array_equal(_np(traj["edge"][0]).astype(np.int64), edge)
+    # its reward row comes from the deferred fold's codes (edge >= 4: the arithmetic path)
+    assert np.array_equal(_u64(_np(traj["reward"][0])), _u64(_np(out["reward"])))
 
 
 def test_rollout_does_not_pin_trajectories(mapfx_mod):
@@ -823,3 +825,46 @@ def test_rollout_does_not_pin_trajectories(mapfx_mod):
     n = len(b._traj_cache)
     b.rollout(8, seed=1, traj=traj)
     assert len(b._traj_cache) == n
+
+
+@pytest.mark.parametrize("S,N,E,T,p", [
+    (128, 256, 40, 21, 0.10),   # C5 shape: folds at steps 7, 15 and the partial ring at 20
+    (24, 256, 24, 19, 0.05),    # dense: stacked agents, edge counts >= 4 (codes >= 32)
+    (64, 300, 8, 10, 0.10)])    # APL 2
+def test_generic_rollout_every_step(mapfx_mod, S, N, E, T, p):
+    """Generic-kernel rollouts (one env per block) fold the rewards from per-agent codes
+    every 8 steps; every step's outputs must equal single step launches (per-step fold),
+    bit for bit, including an env whose step 9 is skipped for an invalid action."""
+    from mapfx.maps import synthetic_instances
+    inst = synthetic_instances(E, S, S, N, p_obstacle=p, seed=17)
+    kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=2000, obs=("window_occ",), window=5)
+    b1 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
+    b2 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
+    b1.reset()
+    b2.reset()
+    acts = b2.gen_actions(T, 5, t0=0).to(torch.int32)
+    acts[9, 2, 0] = 7                            # env 2 skips step 9
+    traj = b1.rollout(T, actions=acts)
+    with pytest.raises(AssertionError):
+        b1.check_err()
+    max_edge = 0
+    for k in range(T):
+        out = b2.step(acts[k])
+        if k == 9:
+            with pytest.raises(AssertionError):
+                b2.check_err()
+        for key in ("reward", "reward_f32", "term", "node", "edge", "avail", "obs_window_occ"):
+            if key not in out:
+                continue
+            x, y = _np(out[key]), _np(traj[key][k])
+            if x.dtype == np.float64:
+                assert np.array_equal(_u64(x), _u64(y)), (key, k)
+            else:
+                assert np.array_equal(x, y), (key, k)
+        max_edge = max(max_edge, int(_np(out["edge"]).max()))
+        assert np.array_equal(_np(traj["traj_pos"][k]), _np(b2.pos)), k
+        assert np.array_equal(_np(traj["traj_t"][k]), _np(b2.t)), k
+    assert int(_np(traj["traj_t"][9])[2]) == int(_np(traj["traj_t"][8])[2])
+    if S == 24:
+        assert max_edge >= 4, max_edge
+    assert np.array_equal(_np(b1.steps), _np(b2.steps))

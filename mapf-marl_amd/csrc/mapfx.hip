@@ -251,7 +251,7 @@ __device__ __forceinline__ __attribute__((unused)) uint32_t lds_addr(const void*
 #define MAPFX_FOLD_R 8  // deferred-fold ring depth of the generic rollout (power of two; 0 = off)
 #endif
 #ifndef MAPFX_OCC_U
-#define MAPFX_OCC_U 0   // rows in flight per thread in write_occ16_rows (0: by window size)
+#define MAPFX_OCC_U 1   // rows in flight per thread in write_occ16_rows (0: 4 at W <= 5, else 2)
 #endif
 #ifndef MAPFX_W0_WRITES
 #define MAPFX_W0_WRITES 1  // wave 0 writes window records on the steps without a fold
@@ -430,6 +430,36 @@ __device__ void write_occ16_rows(const Geo& g, const unsigned char* lds, const i
 // window / avail / reward path alone (FEAT 0) keeps its register budget <= 128
 // VGPRs, i.e. 4 blocks of 256 threads per CU.
 // ---------------------------------------------------------------------------
+#ifdef MAPFX_STAMPS
+// Diagnostic build only (never the shipped library): per-segment s_memtime stamps
+// of block 0 / lane 0, read back with mapfx_debug_stamps().
+__device__ unsigned long long g_stamps[256 * 8];
+#define STAMP(k)                                                                  \
+  do {                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    unsigned long long t_;                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && s < 256) g_stamps[s * 8 + (k)] = t_; \
+  } while (0)
+// prologue / epilogue stamps of block 0 / lane 0 (row 255 of g_stamps)
+#define PSTAMP(k)                                                                 \
+  do {                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    unsigned long long t_;                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
+    __builtin_amdgcn_sched_barrier(0);                                            \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[255 * 8 + (k)] = t_;       \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#define PSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 constexpr int FEAT_PRIM = 1, FEAT_FULL = 2;
 
 // The fp64 reward of one agent from its reward code (deferred fold): bit 0 counted
@@ -544,6 +574,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
           act_nx[k] = load_action(a.actions, a.act_dtype,
                                   ((long long)(s + 1) * Elong + env) * N + lane + k * g.L);
     }
+    STAMP(0);
     // ================= P0: move decision on the PRE-step map =================
     int oc[APL], nc[APL], act[APL], pre[APL];
     bool moved[APL], envc[APL];
@@ -583,6 +614,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       }
     }
     lds_barrier();  // B1: every pre-step map read is done
+    STAMP(1);
     // ================= P1: move the agent counts =================
     const bool skip = (fl[1] != 0) || !a.do_step;
 #pragma unroll
@@ -602,7 +634,13 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       if constexpr ((FEAT & FEAT_PRIM) != 0) rcs[ag] = (r[k] << 16) | (c[k] & 0xFFFF);
     }
     if (a.do_step && !skip && env_ok) ++tcur;
+    if (lane == 0) {  // the next step's flags: every read of them (step s - 1's) precedes B1
+      int* nf = flag + ((s + 1) & 1) * 4;
+      nf[0] = 1;
+      nf[1] = 0;
+    }
     lds_barrier();  // B2: post-step map complete
+    STAMP(2);
     // ================= P2: collisions, rewards, avail, observations =================
     const long long slotE = ROLL ? (long long)s * Elong : 0;  // trajectory slot offset (envs)
     // edge collisions (:364-383): i moved into a cell that had pre-step occupants;
@@ -651,6 +689,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         }
       }
     }
+    STAMP(3);
 #pragma unroll
     for (int k = 0; k < APL; ++k) {
       if (!has[k]) continue;
@@ -744,10 +783,8 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       }
       if (a.term) a.term[slotE + env] = alldone ? 1 : 0;
       if (a.traj_t) a.traj_t[slotE + env] = tcur;
-      int* nf = flag + ((s + 1) & 1) * 4;
-      nf[0] = 1;
-      nf[1] = 0;
     };
+    STAMP(4);
     // ---- deferred fold: lane i < FR of wave 0 folds the code row of step s0 + i ----
     const bool fstep = FR && (((s & (FR - 1)) == FR - 1) || s + 1 == T);
     auto fold_ring = [&]() {
@@ -756,15 +793,44 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       const uint16_t* cs = codes + tid * (g.code_pitch >> 1);
       auto val = [&](uint32_t c) { return c < 32u ? ctab[c] : code_reward(g, c); };
       double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
+      // groups of 8 codes, software-pipelined: while group q is added, group q + 1's
+      // table reads and group q + 2's code read are in flight (codes >= 32, i.e. edge
+      // >= 4, read a clamped entry and are recomputed at the add), so the adds wait on
+      // nothing but the chain
+      const int ng = N >> 3;
       int j = 0;
-      for (; j + 8 <= N; j += 8) {
-        const uint4 v = *(const uint4*)(cs + j);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      if (ng > 0) {
+        const uint4* cs4 = (const uint4*)cs;
+        auto code = [](const uint4& v, int i) {
+          const uint32_t w = i < 2 ? v.x : i < 4 ? v.y : i < 6 ? v.z : v.w;
+          return (w >> (16 * (i & 1))) & 0xFFFFu;
+        };
+        double tv[8], cur[8];
+        uint4 c0 = cs4[0], c1 = ng > 1 ? cs4[1] : c0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          R = R + val(w[i] & 0xFFFFu);
-          R = R + val(w[i] >> 16);
+        for (int i = 0; i < 8; ++i) tv[i] = ctab[min(code(c0, i), 31u)];
+        for (int q = 0; q < ng; ++q) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) cur[i] = tv[i];
+          const uint4 cw = c0;
+          if (q + 1 < ng) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) tv[i] = ctab[min(code(c1, i), 31u)];
+            c0 = c1;
+            if (q + 2 < ng) c1 = cs4[q + 2];
+          }
+          if ((cw.x | cw.y | cw.z | cw.w) & 0xFFE0FFE0u) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              const uint32_t c = code(cw, i);
+              R = R + (c < 32u ? cur[i] : code_reward(g, c));
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) R = R + cur[i];
+          }
         }
+        j = ng << 3;
       }
       for (; j < N; ++j) R = R + val(cs[j]);
       const long long ri = (long long)(s0 + tid) * Elong + env;
@@ -774,15 +840,18 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     // One env per block over four waves (N > 128): wave 0 runs the tail (the fold is
     // one dependent chain of N adds) while waves 1-3 write the window records; with
     // the deferred fold, wave 0 writes records too except on the fold steps.
+    // Without a fold in this step the tail waits until after B3 (no B2b).
     const bool ovl = g.L == 256 && (a.obs_window || a.obs_window_occ);
-    if (ovl) {
+    const bool tail_early = ovl && (!FR || fstep || !MAPFX_W0_WRITES);
+    if (tail_early) {
       lds_barrier();  // B2b: rew[] / codes and the alldone flag complete
       if (tid < 64) {
         lane0_tail(fl[0] != 0);
         if (fstep) fold_ring();
       }
     }
-    const int wt0 = (ovl && (!FR || fstep || !MAPFX_W0_WRITES)) ? 64 : 0;  // first writer thread
+    const int wt0 = tail_early ? 64 : 0;  // first writer thread
+    STAMP(5);
     if ((a.obs_window || a.obs_window_occ) && !(MAPFX_GABL & 2) && tid >= wt0) {  // :323-342
       const int wtid = tid - wt0, wnt = g.BT - wt0;
       const int nenv = min(g.EPB, g.E - env0);
@@ -886,10 +955,12 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         }
       }
     }
+    STAMP(6);
     lds_barrier();  // B3: rew[] and flags complete
+    STAMP(7);
     // ================= P3: fold, term, staging copy-out, autoreset =================
     const bool alldone = fl[0] != 0;
-    if (!ovl) {
+    if (!tail_early) {
       lane0_tail(alldone);
       if (fstep && tid < 64) fold_ring();
     }
@@ -912,10 +983,10 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       }
     }
     if (a.autoreset && alldone && a.do_step) tcur = 0;
-    // B4: the autoreset's map atomics, and (without the overlap) the tail's reset of the
-    // next step's flags, before the next step; with the overlap and no autoreset every
-    // hand-off of this step is already ordered by B3
-    if (ROLL && s + 1 < T && (a.autoreset || !ovl)) lds_barrier();
+    // B4: the autoreset's map atomics before the next step's reads; without autoreset
+    // every hand-off of this step is already ordered by B3 (the tail and the fold read
+    // nothing the next step writes before its B1)
+    if (ROLL && s + 1 < T && a.autoreset) lds_barrier();
   }
 
   // ---- write back the env state ----
@@ -957,35 +1028,6 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
 // Diagnostic build only: per-wave shader-clock / 100 MHz real-time clock at the
 // start and end of the step loop, read back with mapfx_debug_clocks().
 __device__ unsigned long long g_clk[8 * 32768];
-#endif
-#ifdef MAPFX_STAMPS
-// Diagnostic build only (never the shipped library): per-segment s_memtime stamps
-// of block 0 / lane 0, read back with mapfx_debug_stamps().
-__device__ unsigned long long g_stamps[256 * 8];
-#define STAMP(k)                                                                  \
-  do {                                                                            \
-    __builtin_amdgcn_sched_barrier(0);                                            \
-    unsigned long long t_;                                                        \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
-    __builtin_amdgcn_sched_barrier(0);                                            \
-    if (blockIdx.x == 0 && threadIdx.x == 0 && s < 256) g_stamps[s * 8 + (k)] = t_; \
-  } while (0)
-// prologue / epilogue stamps of block 0 / lane 0 (row 255 of g_stamps)
-#define PSTAMP(k)                                                                 \
-  do {                                                                            \
-    __builtin_amdgcn_sched_barrier(0);                                            \
-    unsigned long long t_;                                                        \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");  \
-    __builtin_amdgcn_sched_barrier(0);                                            \
-    if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[255 * 8 + (k)] = t_;       \
-  } while (0)
-#else
-#define STAMP(k) \
-  do {           \
-  } while (0)
-#define PSTAMP(k) \
-  do {            \
-  } while (0)
 #endif
 
 // Wave-path cell format: one byte per padded cell = (obstacle << 7) | c with

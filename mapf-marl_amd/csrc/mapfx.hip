@@ -504,6 +504,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   const int FR = (ROLL && a.do_step) ? g.fold_R : 0;
   uint16_t* codes = (uint16_t*)(lds + g.off_rew);
   double* ctab = (double*)(lds + g.off_ctab);  // code_reward of the codes < 32
+  int* bigrow = (int*)(ctab + 32);              // ring row holds a code >= 32 (edge >= 4)
 
   // ---- per-lane agent state (registers) ----
   int r[APL], c[APL], gr[APL], gc[APL], st[APL];
@@ -537,6 +538,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   }
   for (int i = lane; i < 8; i += g.L) flag[i] = (i & 3) == 0 ? 1 : 0;  // alldone = 1, bad = 0
   if (FR && tid < 32) ctab[tid] = code_reward(g, (uint32_t)tid);
+  if (FR && tid < FR) bigrow[tid] = 0;
   __syncthreads();
   fill_map<CellT>(g, map32, bitsL, lane);
   __syncthreads();
@@ -706,6 +708,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
           codes[(s & (FR - 1)) * (g.code_pitch >> 1) + ag] =
               (uint16_t)((dn[k] ? 0u : 1u) | (envc[k] ? 2u : 0u) | ((uint32_t)node << 2) |
                          ((uint32_t)edge << 3));
+          if (edge >= 4) bigrow[s & (FR - 1)] = 1;  // the fold takes this row's slow path
           if (!dn[k]) ++st[k];
         } else {
           double rr = 0.0;  // :94-130, exact fp64 op order
@@ -793,45 +796,41 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       const uint16_t* cs = codes + tid * (g.code_pitch >> 1);
       auto val = [&](uint32_t c) { return c < 32u ? ctab[c] : code_reward(g, c); };
       double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
-      // groups of 8 codes, software-pipelined: while group q is added, group q + 1's
-      // table reads and group q + 2's code read are in flight (codes >= 32, i.e. edge
-      // >= 4, read a clamped entry and are recomputed at the add), so the adds wait on
-      // nothing but the chain
-      const int ng = N >> 3;
+      // Rows with only codes < 32 (edge <= 3): groups of 8 codes, software-pipelined
+      // over two register sets -- while group q is added, group q + 1's table reads and
+      // group q + 2's code read are in flight -- so the adds wait on nothing but the
+      // chain.  A row with a larger edge count takes the plain loop below.
+      const int ng = bigrow[tid] ? 0 : N >> 3;
       int j = 0;
       if (ng > 0) {
         const uint4* cs4 = (const uint4*)cs;
-        auto code = [](const uint4& v, int i) {
-          const uint32_t w = i < 2 ? v.x : i < 4 ? v.y : i < 6 ? v.z : v.w;
-          return (w >> (16 * (i & 1))) & 0xFFFFu;
+        auto tab = [&](const uint4& v, double (&t)[8]) {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int i = 0; i < 8; ++i) t[i] = ctab[(w[i >> 1] >> (16 * (i & 1))) & 31u];
         };
-        double tv[8], cur[8];
-        uint4 c0 = cs4[0], c1 = ng > 1 ? cs4[1] : c0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) tv[i] = ctab[min(code(c0, i), 31u)];
-        for (int q = 0; q < ng; ++q) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) cur[i] = tv[i];
-          const uint4 cw = c0;
+        double tA[8], tB[8];
+        uint4 cA = cs4[0], cB = cs4[ng > 1 ? 1 : 0];
+        tab(cA, tA);
+        for (int q = 0; q < ng; q += 2) {
           if (q + 1 < ng) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) tv[i] = ctab[min(code(c1, i), 31u)];
-            c0 = c1;
-            if (q + 2 < ng) c1 = cs4[q + 2];
+            tab(cB, tB);
+            if (q + 2 < ng) cA = cs4[q + 2];
           }
-          if ((cw.x | cw.y | cw.z | cw.w) & 0xFFE0FFE0u) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              const uint32_t c = code(cw, i);
-              R = R + (c < 32u ? cur[i] : code_reward(g, c));
+          for (int i = 0; i < 8; ++i) R = R + tA[i];
+          if (q + 1 < ng) {
+            if (q + 2 < ng) {
+              tab(cA, tA);
+              if (q + 3 < ng) cB = cs4[q + 3];
             }
-          } else {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) R = R + cur[i];
+            for (int i = 0; i < 8; ++i) R = R + tB[i];
           }
         }
         j = ng << 3;
       }
+      bigrow[tid] = 0;
       for (; j < N; ++j) R = R + val(cs[j]);
       const long long ri = (long long)(s0 + tid) * Elong + env;
       if (a.reward) a.reward[ri] = R;
@@ -2913,7 +2912,7 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   if (MAPFX_FOLD_R > 0 && EPB == 1 && L >= 64 && std::isfinite(c.step_reward) && std::isfinite(c.collide_reward)) {
     constexpr int FOLD_R = MAPFX_FOLD_R;
     const int ring = std::max(rew_bytes, FOLD_R * g.code_pitch);
-    const int lds_f = g.gen_lds - rew_bytes + ring + 32 * 8;
+    const int lds_f = g.gen_lds - rew_bytes + ring + 32 * 8 + FOLD_R * 4;
     if (LDS_MAX / lds_f >= LDS_MAX / g.gen_lds) {
       g.fold_R = FOLD_R;
       g.off_flag = g.off_rew + ring;

@@ -5,7 +5,7 @@
 # the C5 per-phase stamps.
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r03ah
+OUT=gpurun_out/r03ai
 mkdir -p $OUT
 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
   -k "rollout or stacked or invalid or autoreset" > $OUT/tests.txt 2>&1 || { tail -40 $OUT/tests.txt; exit 1; }

@@ -64,11 +64,13 @@ def parse():
                     help="target CPU work of the cpu_baseline sample (0 disables)")
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: skip the RCCL gather leg (reported beside the compute-only value)")
-    ap.add_argument("--gather-payload", default="occ", choices=("occ", "planes", "reward_done"),
+    ap.add_argument("--gather-payload", default="occ",
+                    choices=("occ", "planes", "reward_done", "compact"),
                     help="what each chunk gathers to rank 0: occ = obs_window_occ (the window as "
                          "one occupancy plane, half the bytes of the two planes) + reward + done; "
                          "planes = obs_window + reward + done; reward_done = reward + done only "
-                         "(observations consumed on-rank)")
+                         "(observations consumed on-rank); compact = reward + u16 cell + done bit "
+                         "per agent-step (rank 0 rebuilds observations with mapfx_observe)")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank launch + shard + packed gather")
     ap.add_argument("--selftest-envs", type=int, default=6)
@@ -360,6 +362,10 @@ def main():
         torch.cuda.synchronize()
         eager_ms = (time.perf_counter() - t2) / ks * 1e3
         cb = canonical_bytes_per_env_step(S, S, N, W)
+        # HBM bytes per launch of the per-step kernel from its own PMC profile
+        # (profiles/pmc_<config>_step.json, taken of this bench command)
+        ptraffic, ptraffic_src = profile_traffic("%s_step" % args.config, config=args.config + "_step",
+                                                 T=1, E=E)
         per_step = {
             "value": round(E * N * reps * ks / pel * world, 1),
             "ms_per_step": round(pel / (reps * ks) * 1e3, 5),
@@ -369,7 +375,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(E * cb / (pk_ms * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(E * cb / (pk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "bytes_per_env_step": cb},
+                         "traffic": ptraffic, "traffic_source": ptraffic_src,
+                         "bytes_per_env_step": cb, "bytes_per_launch": E * cb},
         }
 
     # ---- RCCL gather of (obs, reward, done) to rank 0 (N > 1: on by default) ----
@@ -378,6 +385,9 @@ def main():
         gb, gouts, gkeys = b, outs, (wkey, "reward", "traj_done")
         if args.gather_payload == "reward_done":
             gkeys = ("reward", "traj_done")
+        elif args.gather_payload == "compact":
+            from mapfx.dist import COMPACT_KEYS
+            gkeys = COMPACT_KEYS
         elif args.gather_payload == "occ" and wkind != "window_occ":
             gb = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
                                      episode_limit=limit, obs=("window_occ",), window=W,
@@ -462,6 +472,7 @@ def main():
 
 # rank 0's xGMI ingress: 7 peers x one ~153 GB/s link each
 XGMI_LINK_GBS = 153.0
+GATHER_MIN_CHUNKS = 3
 
 
 def time_gather(dist, b, acts, outs, T, k0, K, world, E, N, keys, payload):
@@ -472,13 +483,20 @@ def time_gather(dist, b, acts, outs, T, k0, K, world, E, N, keys, payload):
     gather (stream wait, no sync).  The ingress bound: rank 0 receives (world - 1)
     chunks per chunk time over at most (world - 1) links."""
     from mapfx.dist import OverlappedGather
-    og = OverlappedGather(b, T, keys=keys, outputs=outs)
+    og = OverlappedGather(b, T, keys=keys, outputs=outs, compact=(payload == "compact"))
     og.step_chunk(actions=acts[:T])                  # warm the communicator
     og.result(0)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
-    nch = K // T
+    # at least GATHER_MIN_CHUNKS chunks whatever --steps is: with one chunk the
+    # double-buffered overlap (chunk i + 1 computing while chunk i travels) would
+    # never be what gets timed
+    nch = max(GATHER_MIN_CHUNKS, K // T)
+    if acts.shape[0] < k0 + nch * T:                 # more inputs, resident before timing
+        acts = b.gen_actions(k0 + nch * T, seed=2)
+        torch.cuda.synchronize()
+        dist.barrier()
     t0 = time.perf_counter()
     for i in range(nch):
         og.step_chunk(actions=acts[k0 + i * T:k0 + (i + 1) * T])
@@ -704,7 +722,9 @@ def run_primal(args, dist, rank, world, local):
     bpc = primal_bytes_per_call(s_obs)
     launch_bytes = E * (KC * bpc + (8 + 8 + 8) * N + inst["bits"].shape[1])  # + pos/goal in, pos out
     achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
-    traffic, traffic_src = profile_traffic("primal", E=E, N=N, K=KC, s=s_obs)
+    # the profile is keyed by what tools/pmc_traffic.py records: config, calls per launch
+    # (T) and worlds (E); the bench's fixed 32 x 32 / 16 agents / s = 10 shape is implied
+    traffic, traffic_src = profile_traffic("primal", config="primal", E=E, T=KC)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         from oracle.primal_dyn_oracle import PrimalWorld

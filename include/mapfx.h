@@ -180,6 +180,16 @@ int mapfx_rollout_timed(mapfx_t* h, const mapfx_state* st, int32_t T, const void
 int mapfx_gen_actions(mapfx_t* h, uint64_t seed, int32_t t0, int32_t T, int8_t* out,
                       void* stream);
 
+/* Compact copy of a rollout's trajectory for the gather to rank 0
+ * (runners/parallel_runner.py:117-173: the parent collects every env's state each
+ * step): cell[T][E][N] = row * W + col of traj_pos (u16; needs H*W <= 65536) and
+ * done_bits[T][E][ceil(N/8)] with bit (a & 7) of byte a >> 3 = traj_done[..][a].
+ * Together with the env's reward this is the state the obs follow from: rank 0
+ * rebuilds any step's window / full / PRIMAL observation with mapfx_observe on the
+ * unpacked positions.  ABI 3 addition. */
+int mapfx_pack_compact(mapfx_t* h, int32_t T, const int32_t* traj_pos, const uint8_t* traj_done,
+                       uint16_t* cell, uint8_t* done_bits, void* stream);
+
 /* The action generator (host reference of the device one):
  * splitmix64(seed ^ env*0xD1B54A32D192ED03 ^ t*0xABC98388FB8FAC03
  *            ^ agent*0x8CB92BA72F3D8DD7) % 5 */

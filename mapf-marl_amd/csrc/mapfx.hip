@@ -2551,6 +2551,27 @@ __global__ void gen_actions_kernel(long long total, int E, int N, long long env_
   out[i] = (int8_t)gen_action(seed, env_offset + e, t0 + tt, ag);
 }
 
+// Compact gather payload (mapfx_pack_compact): every agent-step's (row, col) as the
+// u16 cell index row * W + col, and the dones as bits.  Thread i owns agent-step i
+// of the [T][E][N] trajectory (coalesced 8-B reads, 2-B writes); the thread of agent
+// 8k of an env-step packs the done bytes of agents 8k..8k+7 (L1 hits: its neighbours
+// read the same line) into bit 0..7 of that env-step's byte k.
+__global__ void pack_compact_kernel(long long total, int N, int W, int nbytes, const int2* traj_pos,
+                                    const uint8_t* traj_done, uint16_t* cell, uint8_t* done_bits) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int2 p = traj_pos[i];
+  cell[i] = (uint16_t)(p.x * W + p.y);
+  const long long es = i / N;
+  const int ag = (int)(i - es * N);
+  if ((ag & 7) == 0) {
+    uint32_t b = 0;
+    const int m = min(8, N - ag);
+    for (int k = 0; k < m; ++k) b |= (traj_done[i + k] ? 1u : 0u) << k;
+    done_bits[es * nbytes + (ag >> 3)] = (uint8_t)b;
+  }
+}
+
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
 uint64_t magic48(int d) { return ((1ull << 48) + (uint64_t)d - 1) / (uint64_t)d; }
@@ -3145,6 +3166,23 @@ int mapfx_gen_actions(mapfx_t* h, uint64_t seed, int32_t t0, int32_t T, int8_t* 
                      (hipStream_t)stream, total, h->geo.E, h->geo.N, (long long)h->geo.env_offset,
                      seed, t0, out);
   return check_hip(hipGetLastError(), "gen_actions_kernel launch");
+}
+
+int mapfx_pack_compact(mapfx_t* h, int32_t T, const int32_t* traj_pos, const uint8_t* traj_done,
+                       uint16_t* cell, uint8_t* done_bits, void* stream) {
+  if (!h) return set_error(MAPFX_EINVAL, "NULL handle");
+  if (T < 0) return set_error(MAPFX_EINVAL, "T < 0");
+  if ((long long)h->cfg.H * h->cfg.W > 65536)
+    return set_error(MAPFX_EINVAL, "compact cells are u16: H*W = %lld > 65536",
+                     (long long)h->cfg.H * h->cfg.W);
+  const long long total = (long long)T * h->geo.E * h->geo.N;
+  if (total == 0) return MAPFX_OK;
+  if (!traj_pos || !traj_done || !cell || !done_bits) return set_error(MAPFX_EINVAL, "NULL buffer");
+  const int bt = 256;
+  hipLaunchKernelGGL(pack_compact_kernel, dim3((unsigned)((total + bt - 1) / bt)), dim3(bt), 0,
+                     (hipStream_t)stream, total, h->geo.N, h->cfg.W, (h->geo.N + 7) / 8,
+                     (const int2*)traj_pos, traj_done, cell, done_bits);
+  return check_hip(hipGetLastError(), "pack_compact_kernel launch");
 }
 
 }  // extern "C"

@@ -1323,7 +1323,15 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
     delete h;
     return perr(MAPFX_EINVAL, "one env needs more than 160 KB of LDS (map too large)");
   }
-  if (g.big && (g.wg_lds > 160 * 1024 || g.huge_lds > 160 * 1024)) {
+  if (g.big && g.huge_lds > 160 * 1024) {
+    char msg[200];
+    snprintf(msg, sizeof msg,
+             "MARL_PARTIAL: the %d x %d map's BFS frontier needs H * ceil(W / 64) * 8 = %d B of "
+             "LDS (> 160 KB: H * ceil(W / 64) must be <= 20480)", c.H, c.W, g.huge_lds);
+    delete h;
+    return perr(MAPFX_EINVAL, msg);
+  }
+  if (g.big && g.wg_lds > 160 * 1024) {
     delete h;
     return perr(MAPFX_EINVAL, "MARL_PARTIAL: the workgroup path needs more than 160 KB of LDS");
   }

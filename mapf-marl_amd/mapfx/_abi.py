@@ -90,6 +90,7 @@ EXPORTS = ("mapfx_abi_version", "mapfx_last_error", "mapfx_map_stride", "mapfx_o
            "mapfx_edge_elem_size",
            "mapfx_create", "mapfx_destroy", "mapfx_query", "mapfx_reset", "mapfx_step",
            "mapfx_observe", "mapfx_rollout", "mapfx_rollout_timed", "mapfx_gen_actions", "mapfx_action",
+           "mapfx_pack_compact",
            "mapfx_partial_create", "mapfx_partial_destroy", "mapfx_partial_obs_dim",
            "mapfx_partial_goal_dist_elem_size",
            "mapfx_partial_goal_dist", "mapfx_partial_reset", "mapfx_partial_step",
@@ -141,6 +142,7 @@ def _load():
                                         P(Out), c_vp, c_vp, c_vp]),
         "mapfx_gen_actions": (c_i32, [c_vp, c_u64, c_i32, c_i32, c_vp, c_vp]),
         "mapfx_action": (c_i32, [c_u64, c_i64, c_i32, c_i32]),
+        "mapfx_pack_compact": (c_i32, [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
         "mapfx_partial_create": (c_i32, [P(PCfg), P(c_vp)]),
         "mapfx_partial_destroy": (None, [c_vp]),
         "mapfx_partial_obs_dim": (c_i32, [c_vp]),

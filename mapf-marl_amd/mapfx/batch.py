@@ -305,6 +305,39 @@ class MapfGridBatch:
                                         ptr(out), _stream_handle()), "mapfx_gen_actions")
         return out
 
+    def pack_compact(self, traj_pos, traj_done, cell, done_bits):
+        """cell[T,E,N] (int16 holding the u16 row * W + col) and done_bits
+        [T,E,ceil(N/8)] (bit a & 7 of byte a >> 3) from a rollout's traj_pos /
+        traj_done, on the current stream (mapfx_pack_compact)."""
+        T = int(traj_pos.shape[0])
+        nb = (self.N + 7) // 8
+        for name, t, shape, dt in (("traj_pos", traj_pos, (T, self.E, self.N, 2), torch.int32),
+                                   ("traj_done", traj_done, (T, self.E, self.N), torch.uint8),
+                                   ("cell", cell, (T, self.E, self.N), torch.int16),
+                                   ("done_bits", done_bits, (T, self.E, nb), torch.uint8)):
+            if tuple(t.shape) != shape or t.dtype != dt or not t.is_contiguous() \
+                    or t.device != self.device:
+                raise ValueError("%s must be a contiguous %s %s tensor on %s"
+                                 % (name, shape, dt, self.device))
+        check(self._call(lib.mapfx_pack_compact, self._h, T, ptr(traj_pos), ptr(traj_done),
+                         ptr(cell), ptr(done_bits)), "mapfx_pack_compact")
+
+    def set_positions(self, pos, done=None, t=None):
+        """Overwrite the device state (pos [E,N,2] int32 (row, col), optional done /
+        t) -- e.g. positions unpacked from a compact gather, to rebuild their
+        observations with observe().  Positions are checked to lie on the grid (one
+        host sync): the kernels index their LDS cell maps with them."""
+        p = torch.as_tensor(pos, device=self.device).view(self.E, self.N, 2)
+        lo = torch.tensor([0, 0], device=self.device)
+        hi = torch.tensor([self.H, self.W], device=self.device)
+        if p.numel() and not bool(((p >= lo) & (p < hi)).all()):
+            raise ValueError("positions outside the %dx%d grid" % (self.H, self.W))
+        self.pos.copy_(p)
+        if done is not None:
+            self.done.copy_(torch.as_tensor(done, device=self.device).view(self.E, self.N))
+        if t is not None:
+            self.t.copy_(torch.as_tensor(t, device=self.device).view(self.E))
+
     def host_mirror(self):
         """Pinned host copy of the packed buffer and its typed views (packed=True)."""
         if not self.packed:

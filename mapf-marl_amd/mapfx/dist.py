@@ -112,6 +112,44 @@ class ChunkLayout:
         return out
 
 
+COMPACT_KEYS = ("reward", "cell", "done_bits")
+
+
+def compact_spec(T, E, N):
+    """The compact gather payload of a T-step chunk of E envs of N agents: the env
+    rewards (f64, the runner's reward row) and, per agent-step, the u16 cell index
+    row * W + col (held in int16) and the done flag as one bit (the
+    observations follow from the positions and the static maps, so rank 0 rebuilds
+    the ones it needs with mapfx_observe -- unpack_compact)."""
+    T, E, N = int(T), int(E), int(N)
+    return {"reward": ((T, E), torch.float64), "cell": ((T, E, N), torch.int16),
+            "done_bits": ((T, E, (N + 7) // 8), torch.uint8)}
+
+
+def pack_compact_host(traj_pos, traj_done, W, cell, done_bits):
+    """mapfx_pack_compact for CPU tensors (the gloo tests' oracle stand-in batch;
+    device batches use the HIP kernel)."""
+    c = traj_pos[..., 0] * int(W) + traj_pos[..., 1]
+    cell.copy_(c.to(torch.int32).to(torch.int16))
+    N = traj_done.shape[-1]
+    nb = done_bits.shape[-1]
+    pad = torch.zeros(traj_done.shape[:-1] + (nb * 8,), dtype=torch.int32)
+    pad[..., :N] = (traj_done != 0).to(torch.int32)
+    w = torch.tensor([1 << k for k in range(8)], dtype=torch.int32)
+    done_bits.copy_((pad.view(traj_done.shape[:-1] + (nb, 8)) * w).sum(-1).to(torch.uint8))
+
+
+def unpack_compact(views, W, N):
+    """Gathered compact views (key -> [..., T, E, ...]) -> {"reward", "pos" [..., N, 2]
+    int32 (row, col), "done" [..., N] uint8}."""
+    cell = views["cell"].to(torch.int32) & 0xFFFF
+    pos = torch.stack((cell // int(W), cell % int(W)), dim=-1).to(torch.int32)
+    db = views["done_bits"].to(torch.int32)
+    bits = torch.arange(8, device=db.device, dtype=torch.int32)
+    done = ((db.unsqueeze(-1) >> bits) & 1).flatten(-2)[..., :int(N)].to(torch.uint8)
+    return {"reward": views["reward"], "pos": pos, "done": done}
+
+
 class OverlappedGather:
     """Rollout chunks with ONE gather of each chunk's (obs, reward, done) to `dst`.
 
@@ -124,18 +162,30 @@ class OverlappedGather:
         step_chunk(i + 2) never race the overwrite;
       * result(i) makes the current stream wait for chunk i's gather (no host sync).
     On a CPU device (gloo) everything is synchronous on the calling thread.
+
+    compact=True gathers COMPACT_KEYS instead of `keys`: the reward row plus every
+    agent-step's u16 cell and done bit, packed by mapfx_pack_compact on the side
+    stream (about a tenth of the occupancy-window payload).
     """
 
     def __init__(self, batch, T: int, keys=("obs_window", "reward", "traj_done"), outputs=None,
-                 dst: int = 0, group=None):
+                 dst: int = 0, group=None, compact=False):
         import torch.distributed as dist
         self.dist = dist
         self.batch = batch
         self.T = int(T)
+        self.compact = bool(compact)
+        spec = dict(batch.out_spec(self.T))
+        if self.compact:   # the gathered prefix is COMPACT_KEYS, packed from the rollout
+            keys = COMPACT_KEYS
+            spec.update(compact_spec(self.T, batch.E, batch.N))
+            if outputs is not None:
+                outputs = tuple(outputs) + tuple(k for k in ("reward", "traj_pos", "traj_done")
+                                                 if k not in outputs)
         self.keys = tuple(keys)
         self.outputs = outputs
         self.dst, self.group = dst, group
-        self.layout = ChunkLayout(batch.out_spec(self.T), order=self.keys)
+        self.layout = ChunkLayout(spec, order=self.keys)
         # whole 16-B units, so every typed view of a received row stays aligned
         self.gbytes = -(-self.layout.end_of(self.keys) // ChunkLayout.ALIGN) * ChunkLayout.ALIGN
         dev = batch.device
@@ -167,6 +217,10 @@ class OverlappedGather:
         if not self.cuda:
             self.batch.rollout(self.T, actions=actions, seed=seed, t0=t0, traj=self.bufs[cur],
                                outputs=self.outputs)
+            if self.compact:
+                b = self.bufs[cur]
+                pack_compact_host(b["traj_pos"], b["traj_done"], self.batch.W, b["cell"],
+                                  b["done_bits"])
             self._gather(cur)
             self.i += 1
             return i
@@ -179,6 +233,9 @@ class OverlappedGather:
         ready.record(cs)
         with torch.cuda.stream(self.side):
             self.side.wait_event(ready)
+            if self.compact:    # the pack runs beside the next chunk, like the gather
+                b = self.bufs[cur]
+                self.batch.pack_compact(b["traj_pos"], b["traj_done"], b["cell"], b["done_bits"])
             self._gather(cur)
             ev = torch.cuda.Event()
             ev.record(self.side)

@@ -69,6 +69,13 @@ class PrimalBatch:
         self.past = None
         if self.diagonal:
             pp = starts if past is None else np.array(past, dtype=np.int32)
+            # the kernels read past as int2 at [e * N + i] and primal_seq_kernel packs it
+            # as biased u8 (row, col) bytes: shape and bounds are checked here
+            if pp.shape != starts.shape:
+                raise ValueError("past must be [E, N, 2] like the starts, got %s" % (pp.shape,))
+            if pp.size and ((pp[..., 0] < 0).any() or (pp[..., 0] >= self.H).any()
+                            or (pp[..., 1] < 0).any() or (pp[..., 1] >= self.W).any()):
+                raise ValueError("past outside the %dx%d grid" % (self.H, self.W))
             self.past = torch.as_tensor(pp).to(dev).contiguous()
         self._state = _abi.QState(pos=ptr(self.pos), goal=ptr(self.goal), map_bits=ptr(self.bits),
                                   past=ptr(self.past))

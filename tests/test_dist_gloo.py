@@ -176,13 +176,14 @@ class _OracleTrajBatch:
     def __init__(self, inst, S, N, W, offset):
         from oracle import corc
         self.corc = corc
-        self.E, self.N, self.W, self.offset = inst["init_pos"].shape[0], N, W, offset
+        self.E, self.N, self.win, self.offset = inst["init_pos"].shape[0], N, W, offset
+        self.W = S   # grid width (MapfGridBatch.W), what the compact payload's cells use
         self.device = torch.device("cpu")
         self.ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=7,
                                    env_offset=offset, nthreads=1)
 
     def out_spec(self, T):
-        E, N, W = self.E, self.N, self.W
+        E, N, W = self.E, self.N, self.win
         return {"obs_window": ((T, E, N, 2, W, W), torch.int8),
                 "obs_window_occ": ((T, E, N, W, W), torch.int8), "reward": ((T, E), torch.float64),
                 "traj_done": ((T, E, N), torch.uint8), "traj_pos": ((T, E, N, 2), torch.int32)}
@@ -193,7 +194,7 @@ class _OracleTrajBatch:
             a = np.array([[lib.orc_action(seed, self.offset + e, t0 + k, i) for i in range(self.N)]
                           for e in range(self.E)], dtype=np.int32)
             r = self.ob.step(a)
-            o = self.ob.observe(window=self.W, full=False)
+            o = self.ob.observe(window=self.win, full=False)
             traj["reward"][k].copy_(torch.from_numpy(r["reward"]))
             traj["obs_window"][k].copy_(torch.from_numpy(o["obs_window"]))
             ob_, ag_ = o["obs_window"][:, :, 0], o["obs_window"][:, :, 1]   # -> occ = agents - obst
@@ -220,7 +221,7 @@ def _og_worker(rank, world, port, q, keys):
         inst = synthetic_instances(c["E"], c["S"], c["S"], c["N"], p_obstacle=0.1, seed=5,
                                    env_offset=rank * c["E"])
         fb = _OracleTrajBatch(inst, c["S"], c["N"], c["W"], rank * c["E"])
-        og = OverlappedGather(fb, c["T"], keys=keys)
+        og = OverlappedGather(fb, c["T"], keys=keys, compact=(keys == "compact"))
         assert og.bytes_per_chunk() % 16 == 0
         got = []
         for i in range(c["chunks"]):
@@ -238,7 +239,7 @@ def _og_worker(rank, world, port, q, keys):
 
 @pytest.mark.parametrize("keys", [("obs_window", "reward", "traj_done"),
                                   ("obs_window_occ", "reward", "traj_done"),
-                                  ("reward", "traj_done")])
+                                  ("reward", "traj_done"), "compact"])
 def test_overlapped_gather_packed_world2(keys):
     """OverlappedGather at world 2 (gloo): ONE gather per chunk of the packed
     (obs, reward, done) prefix, double-buffered receive side; rank 0's per-chunk
@@ -263,6 +264,14 @@ def test_overlapped_gather_packed_world2(keys):
         traj = {k: torch.zeros(s, dtype=d) for k, (s, d) in fb.out_spec(c["T"]).items()}
         fb.rollout(c["T"], seed=9, t0=i * c["T"], traj=traj)
         g = got[i]
+        if keys == "compact":   # reward row + unpacked cells / done bits == the unsharded run
+            from mapfx.dist import COMPACT_KEYS, unpack_compact
+            assert tuple(g) == COMPACT_KEYS
+            u = unpack_compact({k: torch.from_numpy(v) for k, v in g.items()}, c["S"], c["N"])
+            for k, ref in (("reward", "reward"), ("pos", "traj_pos"), ("done", "traj_done")):
+                merged = np.concatenate(list(u[k].numpy()), axis=1)
+                assert np.array_equal(merged.view(np.uint8), traj[ref].numpy().view(np.uint8)), (i, k)
+            continue
         assert set(g) == set(keys)
         for k in g:
             # [world, T, E_rank, ...] -> [T, world * E_rank, ...]

@@ -38,7 +38,7 @@ def _batch(mapfx, E, offset):
     return b
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, compact):
     import sys
     sys.path[:0] = [REPO, PKG_ROOT]
     import torch.distributed as dist
@@ -52,7 +52,7 @@ def _worker(rank, world, port, q):
         b = _batch(mapfx, C["E"], rank * C["E"])
         outs = ("reward", "term", "node", "edge", "avail", "obs_window_occ", "traj_pos", "traj_done",
                 "traj_t")
-        og = OverlappedGather(b, C["T"], keys=KEYS, outputs=outs)
+        og = OverlappedGather(b, C["T"], keys=KEYS, outputs=outs, compact=compact)
         got = []
         for i in range(C["chunks"]):
             og.step_chunk(seed=C["seed"], t0=i * C["T"])
@@ -66,7 +66,12 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_rank_shards_gather_equals_unsharded():
+@pytest.mark.parametrize("compact", [False, True])
+def test_two_rank_shards_gather_equals_unsharded(compact):
+    """compact=True: the gathered payload is the reward row + u16 cells + done bits
+    (mapfx_pack_compact on the side stream); unpacked it equals the unsharded
+    trajectory, and rank 0 rebuilds every step's window from the unpacked positions
+    with mapfx_observe, bit for bit the window the rollout wrote."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import mapfx
@@ -75,7 +80,7 @@ def test_two_rank_shards_gather_equals_unsharded():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, compact)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=100)
@@ -83,8 +88,23 @@ def test_two_rank_shards_gather_equals_unsharded():
         p.join(timeout=30)
         assert p.exitcode == 0
     full = _batch(mapfx, world * C["E"], 0)
+    obs_b = _batch(mapfx, world * C["E"], 0)      # rank 0's observation rebuilder
     for i in range(C["chunks"]):
         traj = full.rollout(C["T"], seed=C["seed"], t0=i * C["T"])
+        if compact:
+            from mapfx.dist import COMPACT_KEYS, unpack_compact
+            assert tuple(got[i]) == COMPACT_KEYS
+            u = unpack_compact({k: torch.from_numpy(v) for k, v in got[i].items()}, C["S"], C["N"])
+            for k, ref in (("reward", "reward"), ("pos", "traj_pos"), ("done", "traj_done")):
+                merged = np.concatenate(list(u[k].numpy()), axis=1)
+                assert np.array_equal(merged.view(np.uint8), traj[ref].cpu().numpy().view(np.uint8)), (i, k)
+            pos = torch.cat(list(u["pos"]), dim=1)                   # [T, world * E, N, 2]
+            for k in range(C["T"]):
+                obs_b.set_positions(pos[k])
+                o = obs_b.observe()
+                torch.cuda.synchronize()
+                assert torch.equal(o["obs_window_occ"], traj["obs_window_occ"][k]), (i, k)
+            continue
         for k in KEYS:
             merged = np.concatenate(list(got[i][k]), axis=1)      # [world, T, E, ...] -> [T, 2E, ...]
             ref = traj[k].cpu().numpy()

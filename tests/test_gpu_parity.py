@@ -827,19 +827,25 @@ def test_rollout_does_not_pin_trajectories(mapfx_mod):
     assert len(b._traj_cache) == n
 
 
-@pytest.mark.parametrize("S,N,E,T,p", [
-    (128, 256, 40, 21, 0.10),   # C5 shape: folds at steps 7, 15 and the partial ring at 20
-    (24, 256, 24, 19, 0.05),    # dense: stacked agents, edge counts >= 4 (codes >= 32)
-    (64, 300, 8, 10, 0.10)])    # APL 2
-def test_generic_rollout_every_step(mapfx_mod, S, N, E, T, p):
+@pytest.mark.parametrize("S,N,E,T,p,obs", [
+    (128, 256, 40, 21, 0.10, ("window_occ",)),  # C5 shape: folds at steps 7, 15, partial ring at 20
+    (24, 256, 24, 19, 0.05, ("window_occ",)),   # dense: stacked agents, edge counts >= 4 (codes >= 32)
+    (64, 300, 8, 10, 0.10, ("window_occ",)),    # APL 2
+    # the fold placement after B3 (no window writer to overlap it with): no window
+    # outputs at L = 256, and a window at L = 128 with one env per block (the map's LDS)
+    (128, 256, 12, 19, 0.10, ()),
+    (128, 256, 12, 19, 0.10, ("full",)),
+    (160, 100, 10, 12, 0.10, ("window_occ",))])
+def test_generic_rollout_every_step(mapfx_mod, S, N, E, T, p, obs):
     """Generic-kernel rollouts (one env per block) fold the rewards from per-agent codes
     every 8 steps; every step's outputs must equal single step launches (per-step fold),
     bit for bit, including an env whose step 9 is skipped for an invalid action."""
     from mapfx.maps import synthetic_instances
     inst = synthetic_instances(E, S, S, N, p_obstacle=p, seed=17)
-    kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=2000, obs=("window_occ",), window=5)
+    kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=2000, obs=obs, window=5)
     b1 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
     b2 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
+    assert b1.info()["envs_per_block"] == 1      # the deferred-fold layout
     b1.reset()
     b2.reset()
     acts = b2.gen_actions(T, 5, t0=0).to(torch.int32)
@@ -853,7 +859,8 @@ def test_generic_rollout_every_step(mapfx_mod, S, N, E, T, p):
         if k == 9:
             with pytest.raises(AssertionError):
                 b2.check_err()
-        for key in ("reward", "reward_f32", "term", "node", "edge", "avail", "obs_window_occ"):
+        for key in ("reward", "reward_f32", "term", "node", "edge", "avail", "obs_window_occ",
+                    "obs_full"):
             if key not in out:
                 continue
             x, y = _np(out[key]), _np(traj[key][k])

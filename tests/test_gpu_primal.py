@@ -127,7 +127,7 @@ def test_primal_batch_matches_oracle(mapfx_mod, monkeypatch, lanes, H, W, N, s, 
     o = {k: _np(v).copy() for k, v in b.act(ids, acts).items()}
     pos = _np(b.pos)
     b.check_err()
-    for e in list(range(0, E, 16)) + [E - 1]:
+    for e in range(E):     # every world of the batch (the restatement takes < 1 s per world)
         w = PrimalWorld(grids[0 if shared else e], starts[e], goals[e], s, diagonal=diag)
         for k in range(K):
             maps, vec, r, done, mask, on_goal, _, valid = w.step(int(ids[e, k]) - 1, int(acts[e, k]))
@@ -141,26 +141,35 @@ def test_primal_batch_matches_oracle(mapfx_mod, monkeypatch, lanes, H, W, N, s, 
             assert np.array_equal(np.array(w.past), _np(b.past)[e]), e
 
 
-@pytest.mark.parametrize("N", [3, 20, 40])  # 16, 32 and 64 lanes per world (forced)
-def test_primal_bad_call_stops_only_its_world(mapfx_mod, monkeypatch, N):
-    """Worlds share a wave in lane groups: E not a multiple of the worlds per wave,
-    K past one 64-call block, and a bad call in world 2 that ends that world's
-    calls (the reference asserts) while its wave neighbours run on."""
+@pytest.mark.parametrize("N,lanes,s,diag", [
+    (3, "16", 5, False), (20, "16", 5, False), (40, "16", 5, False),  # lane groups (forced)
+    # the host's own choice: even s -> primal_seq_kernel (one world per wave, its
+    # badm / kstop path), s = 4 and 10, and a refused diagonal action 9
+    (3, "", 10, False), (20, "", 4, False), (40, "", 10, False), (20, "", 10, True),
+    (20, "16", 5, True)])
+def test_primal_bad_call_stops_only_its_world(mapfx_mod, monkeypatch, N, lanes, s, diag):
+    """E not a multiple of the worlds per wave, K past one 64-call block, and a bad
+    call in world 2 (an agent id past N, or DIAGONAL_MOVEMENT's action 9) in the second
+    block that ends that world's calls (the reference asserts, :552-557) while the
+    other worlds -- wave neighbours on the lane-group kernel -- run on."""
     from oracle.primal_dyn_oracle import PrimalWorld
-    rng = np.random.default_rng(N)
-    E, H, W, s, K, kbad = 7, 14, 11, 5, 80, 70
+    rng = np.random.default_rng(N + 100 * s + (7 if diag else 0))
+    E, H, W, K, kbad = 7, 14, 11, 80, 70
     grids, starts, goals = _random_worlds(rng, E, H, W, N, 0.1, False)
     ids = rng.integers(1, N + 1, size=(E, K)).astype(np.int32)
-    acts = rng.integers(0, 5, size=(E, K)).astype(np.int32)
-    ids[2, kbad] = N + 1
-    monkeypatch.setenv("MAPFX_PRIMAL_LANES", "16")
-    b = mapfx_mod.PrimalBatch(starts, goals, grids=grids, observation_size=s)
+    acts = rng.integers(0, 9 if diag else 5, size=(E, K)).astype(np.int32)
+    if diag:
+        acts[2, kbad] = 9
+    else:
+        ids[2, kbad] = N + 1
+    monkeypatch.setenv("MAPFX_PRIMAL_LANES", lanes)
+    b = mapfx_mod.PrimalBatch(starts, goals, grids=grids, observation_size=s, diagonal=diag)
     o = {k: _np(v).copy() for k, v in b.act(ids, acts).items()}
     with pytest.raises(AssertionError, match="world 2"):
         b.check_err()
     pos = _np(b.pos)
     for e in range(E):
-        w = PrimalWorld(grids[e], starts[e], goals[e], s)
+        w = PrimalWorld(grids[e], starts[e], goals[e], s, diagonal=diag)
         for k in range(kbad if e == 2 else K):
             maps, vec, r, done, mask, on_goal, _, valid = w.step(int(ids[e, k]) - 1, int(acts[e, k]))
             assert np.float64(r).view(np.uint64) == o["reward"][e, k].view(np.uint64), (e, k)
@@ -169,6 +178,46 @@ def test_primal_bad_call_stops_only_its_world(mapfx_mod, monkeypatch, N):
             assert np.array_equal(maps, o["obs"][e, k]), (e, k)
             assert np.array_equal(vec.view(np.uint64), o["vec"][e, k].view(np.uint64)), (e, k)
         assert np.array_equal(np.array(w.pos), pos[e]), e
+
+
+def test_primal_bench_shape_matches_oracle(mapfx_mod):
+    """bench.py --env primal's shape through the host's kernel choice
+    (primal_seq_kernel): 4096 worlds of 32 x 32 (10 % obstacles), 16 agents, s = 10,
+    64 calls per world in one launch, agents round robin with random actions --
+    every 64th world and the last against the restatement, call by call."""
+    from mapfx.maps import synthetic_instances
+    from oracle.primal_dyn_oracle import PrimalWorld
+    E, S, N, s, K = 4096, 32, 16, 10, 64
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.10, seed=1)
+    b = mapfx_mod.PrimalBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                              observation_size=s)
+    rng = np.random.default_rng(7)
+    ids = np.tile((np.arange(K) % N + 1).astype(np.int32), (E, 1))
+    acts = rng.integers(0, 5, size=(E, K)).astype(np.int32)
+    o = {k: _np(v).copy() for k, v in b.act(torch.from_numpy(ids).cuda(),
+                                             torch.from_numpy(acts).cuda()).items()}
+    pos = _np(b.pos)
+    b.check_err()
+    for e in list(range(0, E, 64)) + [E - 1]:
+        w = PrimalWorld(inst["grid"][e % inst["grid"].shape[0]], inst["init_pos"][e],
+                        inst["goals"][e], s)
+        for k in range(K):
+            maps, vec, r, done, mask, on_goal, _, valid = w.step(int(ids[e, k]) - 1, int(acts[e, k]))
+            assert np.float64(r).view(np.uint64) == o["reward"][e, k].view(np.uint64), (e, k)
+            assert done == bool(o["done"][e, k]) and mask == int(o["next_mask"][e, k]), (e, k)
+            assert on_goal == bool(o["on_goal"][e, k]) and valid == bool(o["valid"][e, k]), (e, k)
+            assert np.array_equal(maps, o["obs"][e, k]), (e, k)
+            assert np.array_equal(vec.view(np.uint64), o["vec"][e, k].view(np.uint64)), (e, k)
+        assert np.array_equal(np.array(w.pos), pos[e]), e
+
+
+def test_primal_rejects_bad_past(mapfx_mod):
+    g = np.zeros((4, 4), np.int8)
+    st, gl = [[[0, 0], [1, 1]]], [[[3, 3], [2, 2]]]
+    for past in ([[[0, 0]]], [[[0, 0], [4, 1]]], [[[0, -1], [1, 1]]]):
+        with pytest.raises(ValueError):
+            mapfx_mod.PrimalBatch(st, gl, grids=g, diagonal=True, past=past)
+    mapfx_mod.PrimalBatch(st, gl, grids=g, diagonal=True, past=[[[0, 1], [1, 2]]])
 
 
 def test_primal_done_when_all_on_goals(mapfx_mod):

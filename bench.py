@@ -545,9 +545,11 @@ def profile_traffic(leg, **match):
 
 def partial_bytes_per_env_step(N, D, HW):
     """Algorithmic HBM bytes of one MARL_PARTIAL env step (state round-trips HBM):
-    reads actions N + state 23N + 13 + goal/init 16N + 2 goal-distance reads 4N +
-    bitmap HW/8; writes obs 4DN + reward 8 + state 12 + avail N + state 23N + 9."""
-    return (N + 23 * N + 13 + 16 * N + 4 * N + HW // 8) + (4 * D * N + 8 + 12 + N + 23 * N + 9)
+    reads actions N + state 27N + 13 (pos 8, steps 4, at_goal 1, done 1, goal_cost 4,
+    node 1, edge 4, carried goal distance 4 per agent) + goal/init 16N + one 2-byte
+    goal-distance read per (moving) agent 2N + bitmap HW/8; writes obs 4DN + reward 8
+    + state 12 + avail N + state 27N + 9."""
+    return (N + 27 * N + 13 + 16 * N + 2 * N + HW // 8) + (4 * D * N + 8 + 12 + N + 27 * N + 9)
 
 
 def run_partial(args, dist, rank, world, local):

@@ -76,6 +76,12 @@ typedef struct mapfx_partial_state {
                                obstacle / unreachable), filled by
                                mapfx_partial_goal_dist; int16, or int32 when H*W >
                                32767 (mapfx_partial_goal_dist_elem_size)            */
+  int32_t* pdist;           /* [E][N] goal_dist of each agent's current cell, carried
+                               from step to step (the reference's _new_pdist / next
+                               _old_pdist, :227-233): a step reads it as opd and looks
+                               up only a moving agent's npd; reset / observe refresh
+                               it from the table.  INT32_MIN (never reset) or a NULL
+                               pointer: looked up.  Appended in ABI 3.            */
 } mapfx_partial_state;
 
 /* Per-call outputs (device, caller-owned; NULL = not produced). */

@@ -1607,11 +1607,22 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
       uint32_t w[4 * NQ];
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
-        const u32x4 v = sl[SLOT_CHUNK * i];
-        w[4 * i] = v.x;
+        // diagnostic 65536: one LDS read of the image (the info chunk) instead of NQ
+        const u32x4 v = sl[(MAPFX_ABLATE & 65536) ? 0 : SLOT_CHUNK * i];
+        w[4 * i] = v.x ^ ((MAPFX_ABLATE & 65536) ? (uint32_t)i : 0u);
         w[4 * i + 1] = v.y;
         w[4 * i + 2] = v.z;
         w[4 * i + 3] = v.w;
+      }
+      if (MAPFX_ABLATE & 262144) {  // diagnostic: the window rows read from the cell map
+        extern __shared__ __align__(16) unsigned char lds_[];
+        const uint32_t* m32 = (const uint32_t*)(lds_ + g.wv_off_map + slot * g.map_env_bytes);
+        const int w0 = ((int)(w[0] & 0xFFFFu) - H2 * g.pitch - H2) >> 2, wpr = g.pitch >> 2;
+#pragma unroll
+        for (int y = 0; y < WIN; ++y) {
+          w[4 + y] = m32[w0 + y * wpr];
+          w[4 + WIN + y] = m32[w0 + y * wpr + 1];
+        }
       }
       const uint32_t* qx = w + 4;
       const int o = ((int)w[0] - H2) & 3;
@@ -2358,6 +2369,10 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
       const int wpr = pitch >> 2;
 #pragma unroll
       for (int y = 0; y < WIN; ++y) {
+        if ((MAPFX_ABLATE & 131072) && (y < H2 - 1 || y > H2 + 1)) {  // diagnostic: the 3 middle rows
+          x[y] = x[WIN + y] = x[2 * WIN + y] = 0x01010101u;
+          continue;
+        }
         x[y] = map32[w0 + y * wpr];
         x[WIN + y] = map32[w0 + y * wpr + 1];
         x[2 * WIN + y] = WIN > 5 ? map32[w0 + y * wpr + 2] : 0u;

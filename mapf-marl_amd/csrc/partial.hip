@@ -25,6 +25,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -75,6 +76,7 @@ struct PArgs {
   int32_t* total_coll;
   const uint8_t* bits;
   const void* gd;  // int16 or int32 (g.gd32)
+  int32_t* pdist;  // [E][N] goal distance of the current cell (carried), or NULL
   const void* actions;
   int act_dtype;
   int do_step;       // 0: observe only
@@ -119,6 +121,24 @@ __device__ inline void wave_fence() {
 __device__ __forceinline__ int goal_dist_at(const PGeo& g, const void* gd, long long oa, int cell) {
   const long long i = oa * g.hw + cell;
   return g.gd32 ? ((const int32_t*)gd)[i] : (int)((const int16_t*)gd)[i];
+}
+
+// The step's goal-path distances (:227-233) with the current cell's distance carried in
+// the state (mapfx_partial_state.pdist, the reference's _new_pdist of the last step):
+// opd is that value, npd = opd unless the agent moved, when it is the table entry of the
+// target cell -- looked up speculatively as soon as the position and action are loaded
+// (the lookup's latency then overlaps the map build).  Every non-step pass (reset,
+// observe: positions may have been rewritten, e.g. by output mode's repair) refreshes
+// the carried value from the table; PD_NONE (a state never reset) falls back to it too.
+constexpr int PD_NONE = (int)0x80000000;
+
+// The move target of action `act` from (r, c) when it lies on the grid (-1 otherwise):
+// the cell whose distance a moving agent's npd is.
+__device__ __forceinline__ int move_target(const PGeo& g, int r, int c, int act) {
+  if (act < 0 || act > 3) return -1;
+  const int tr = r + (act == 0 ? -1 : act == 1 ? 1 : 0);
+  const int tc = c + (act == 2 ? -1 : act == 3 ? 1 : 0);
+  return (tr < 0 || tr >= g.H || tc < 0 || tc >= g.W) ? -1 : tr * g.W + tc;
 }
 
 // ---------------------------------------------------------------------------
@@ -407,6 +427,7 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
   };
 
   int r[APL], c[APL], gr[APL], gc[APL], ir[APL], ic[APL], steps[APL], gcost[APL], edge[APL];
+  int pd[APL];  // goal distance of the current cell (carried, see PD_NONE)
   bool has[APL], at_goal[APL], dn[APL];
   uint32_t node[APL];
   const bool reset_me = a.do_reset && (!a.reset_mask || a.reset_mask[env]);
@@ -423,6 +444,7 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
     has[k] = ag < N;
     r[k] = c[k] = gr[k] = gc[k] = ir[k] = ic[k] = steps[k] = edge[k] = 0;
     gcost[k] = -1;
+    pd[k] = PD_NONE;
     at_goal[k] = dn[k] = false;
     node[k] = 0;
     if (has[k]) {
@@ -440,7 +462,9 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
         gcost[k] = a.goal_cost[oa];
         node[k] = a.node[oa];
         edge[k] = a.edge[oa];
+        if (a.pdist && a.do_step) pd[k] = a.pdist[oa];
       }
+      if (pd[k] == PD_NONE) pd[k] = goal_dist_at(g, a.gd, oa, r[k] * W + c[k]);
     }
   }
   for (int i = tid; i < hs; i += WG_THREADS) {
@@ -516,9 +540,10 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
         dn[k] = true;
       }
       const long long oa = (long long)env * N + ag;
-      const int opd = goal_dist_at(g, a.gd, oa, r[k] * W + c[k]);  // :227-233
-      const int npd = goal_dist_at(g, a.gd, oa, nr[k] * W + ncol[k]);
+      const int opd = pd[k];  // :227-233
+      const int npd = moved[k] ? goal_dist_at(g, a.gd, oa, nr[k] * W + ncol[k]) : opd;
       rew[k] = rew[k] + (double)(opd - npd) / (double)g.limit;
+      pd[k] = npd;
       // the single pre-step occupant's move (0..3, 7: stayed) and the post-step count
       atomicOr(&vals[oslot[k]], (moved[k] ? (uint32_t)act[k] : 7u) << HDEP_SH);
       const int ns = hinsert(keys, g.hs_log, (uint32_t)(nr[k] * W + ncol[k]));
@@ -687,6 +712,7 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
     a.goal_cost[oa] = gcost[k];
     a.node[oa] = (uint8_t)node[k];
     a.edge[oa] = edge[k];
+    if (a.pdist) a.pdist[oa] = pd[k];
   }
   if (tid == 0) {
     a.t[env] = tcur;
@@ -727,6 +753,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   const long long oa = (long long)env * N + ag;
   // ---- state ----
   int r = 0, c = 0, gr = 0, gc = 0, ir = 0, ic = 0, steps = 0, gcost = -1, edge = 0;
+  int pd = PD_NONE;  // goal distance of the current cell (carried)
   bool at_goal = false, dn = false;
   uint32_t node = 0;
   int tcur = 0, total = 0;
@@ -758,7 +785,14 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
       gcost = a.goal_cost[oa];
       node = a.node[oa];
       edge = a.edge[oa];
+      if (a.pdist) pd = a.pdist[oa];
     }
+  }
+  // the step's action, loaded with the state (its lookup below needs it)
+  int act = 4;
+  if (a.do_step && has) {
+    act = load_act(a.actions, a.act_dtype, oa);
+    if (act < 0 || act > 4) act = -1;
   }
   if (reset_me) {
     tcur = 0;
@@ -769,6 +803,16 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   if (env_ok) {
     const uint32_t* src = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)env * g.map_stride));
     for (int w = ag; w < g.bits_words; w += g.L) bitsL[w] = src[w];
+  }
+  // goal-path distances (:227-233): the move target's entry, speculatively (used when the
+  // agent moves), and the current cell's when no carried value applies -- issued here, so
+  // their latency overlaps the map build
+  const bool need_cur = has && (!a.do_step || !a.pdist || pd == PD_NONE);
+  int npd_t = 0;
+  if (has) {
+    const int tgt = (a.do_step && !dn) ? move_target(g, r, c, act) : -1;
+    if (tgt >= 0) npd_t = goal_dist_at(g, a.gd, oa, tgt);
+    if (need_cur) pd = goal_dist_at(g, a.gd, oa, r * g.W + c);
   }
   wave_fence();
   if (env_ok) {
@@ -799,11 +843,6 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
 
   // ---- step (:165-310) ----
   if (a.do_step && env_ok && !(PABL & 2)) {
-    int act = 4;
-    if (has) {
-      act = load_act(a.actions, a.act_dtype, oa);
-      if (act < 0 || act > 4) act = -1;
-    }
     const bool skip = (__ballot(act < 0) & envmask) != 0;  // the reference asserts (:174)
     if (!skip) {
       ++tcur;  // :178
@@ -836,9 +875,10 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
         dn = true;
       }
       if (has) {                                            // :227-233
-        const int opd = goal_dist_at(g, a.gd, oa, r * g.W + c);
-        const int npd = goal_dist_at(g, a.gd, oa, nr * g.W + ncol);
+        const int opd = pd;
+        const int npd = moved ? npd_t : opd;
         rew = rew + (double)(opd - npd) / (double)g.limit;
+        pd = npd;
       }
       // counts move; node / edge collisions (:708-727, :822-857)
       if (has) dep[cur] = (unsigned char)((dep[cur] & 0x80u) | (moved ? (uint32_t)act : 0x7Fu));
@@ -1130,6 +1170,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
     a.goal_cost[oa] = gcost;
     a.node[oa] = (uint8_t)node;
     a.edge[oa] = edge;
+    if (a.pdist) a.pdist[oa] = pd;
   }
   if (env_ok && ag == 0) {
     a.t[env] = tcur;
@@ -1240,6 +1281,7 @@ void fill_state(PArgs& a, const mapfx_partial_state* st) {
   a.total_coll = st->total_coll;
   a.bits = st->map_bits;
   a.gd = st->goal_dist;
+  a.pdist = st->pdist;
 }
 
 void fill_out(PArgs& a, const mapfx_partial_out* o) {
@@ -1319,6 +1361,10 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   // workgroup path keeps no map in LDS)
   int EPW = g.big ? 1 : 64 / L;
   while (EPW > 1 && EPW * per_env > 64 * 1024) --EPW;
+  if (const char* ev = getenv("MAPFX_PARTIAL_EPW")) {  // diagnostic / A-B: fewer envs per wave
+    const int v = atoi(ev);
+    if (v >= 1 && v < EPW) EPW = v;
+  }
   if (!g.big && EPW * per_env > 160 * 1024) {
     delete h;
     return perr(MAPFX_EINVAL, "one env needs more than 160 KB of LDS (map too large)");

@@ -63,7 +63,7 @@ class PCfg(ctypes.Structure):  # include/mapfx_partial.h
 class PState(ctypes.Structure):
     _fields_ = [(k, c_vp) for k in ("pos", "goal", "init_pos", "steps", "at_goal", "done",
                                     "goal_cost", "node", "edge", "t", "terminated", "total_coll",
-                                    "map_bits", "goal_dist")]
+                                    "map_bits", "goal_dist", "pdist")]
 
 
 class POut(ctypes.Structure):

@@ -110,6 +110,9 @@ class MarlPartialBatch:
         self.node = z((E, N), torch.uint8)
         self.edge = z((E, N), torch.int32)
         self.total_coll = z((E,), torch.int32)
+        # goal distance of each agent's current cell, carried by the kernels (INT32_MIN:
+        # not known yet, looked up; reset / observe set it)
+        self.pdist = torch.full((E, N), -2 ** 31, dtype=torch.int32, device=dev)
         gd_dt = torch.int32 if lib.mapfx_partial_goal_dist_elem_size(self.H, self.W) == 4 \
             else torch.int16
         self.goal_dist = z((E, N, self.H * self.W), gd_dt)
@@ -119,7 +122,7 @@ class MarlPartialBatch:
             steps=ptr(self.steps), at_goal=ptr(self.at_goal), done=ptr(self.done),
             goal_cost=ptr(self.goal_cost), node=ptr(self.node), edge=ptr(self.edge), t=ptr(self.t),
             terminated=ptr(self.terminated), total_coll=ptr(self.total_coll),
-            map_bits=ptr(self.bits), goal_dist=ptr(self.goal_dist))
+            map_bits=ptr(self.bits), goal_dist=ptr(self.goal_dist), pdist=ptr(self.pdist))
         self._out = _abi.POut(reward=ptr(self.out["reward"]), obs=ptr(self.out["obs"]),
                               state=ptr(self.out["state"]), avail=ptr(self.out["avail"]),
                               err=ptr(self.err))

@@ -11,3 +11,15 @@ tail -1 $OUT/tests.txt
 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_c2.json 2> $OUT/bench_c2.err \
   || { tail -20 $OUT/bench_c2.err; exit 1; }
 tail -c 600 $OUT/bench_c2.json; echo
+# LDS-traffic ablations of the split kernel (diagnostic builds, results garbage):
+# 2048 step wave writes the info chunk only; 65536 store waves read one chunk;
+# 131072 step wave reads 3 window rows; 262144 store waves read the rows from the map
+bash tools/ab_bench.sh $OUT/ab 2 "--gpus 1 --steps 20 --warmup 5" mapf-marl_amd/mapfx/libmapfx.so \
+  mapf-marl_amd/mapfx/libmapfx_ab2048.so mapf-marl_amd/mapfx/libmapfx_ab65536.so \
+  mapf-marl_amd/mapfx/libmapfx_ab131072.so mapf-marl_amd/mapfx/libmapfx_ab262144.so
+# MARL_PARTIAL per-step kernel: envs per wave 4 (default) / 2 / 1 (more waves per SIMD)
+for epw in 4 2 1 4 2 1; do
+  MAPFX_PARTIAL_EPW=$epw timeout -k 10 200 python3 bench.py --env marl_partial --cpu-seconds 0 \
+    > $OUT/partial_epw$epw.json 2> $OUT/partial_epw$epw.err || { tail -20 $OUT/partial_epw$epw.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$OUT/partial_epw$epw.json')); print('partial EPW $epw', d['kernel_ms_per_step'], d['roofline']['frac'])"
+done

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 4: profiles of what had none: C3's rollout and the per-step
+# drop-in kernel (mapf_wave_kernel<5, false, ...>): trace + FETCH / WRITE + LDS + SQ passes
+# of the bench command each line is taken with, summarised into profiles/.
+set -o pipefail
+export TMPDIR=/tmp
+bash tools/r03_profile.sh r04b_c3 --config c3 --gpus 1 --cpu-seconds 0 --per-step-steps 0 || exit 1
+bash tools/r03_profile.sh r04b_step --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --per-step-steps 200 || exit 1
+O=gpurun_out
+python3 tools/pmc_traffic.py --trace $O/r04b_c3/trace --fetch $O/r04b_c3/pmc_fetch --write $O/r04b_c3/pmc_write \
+  --lds $O/r04b_c3/pmc_lds --sq $O/r04b_c3/pmc_sq --kernel "mapf_wave_kernel<5, true" --config c3 --T 64 --E 2048 \
+  --tag r04_c3 --command "python3 bench.py --config c3 --gpus 1 --cpu-seconds 0 --per-step-steps 0" \
+  --out $O/profiles/pmc_c3.json > /dev/null || exit 1
+python3 tools/pmc_traffic.py --trace $O/r04b_step/trace --fetch $O/r04b_step/pmc_fetch --write $O/r04b_step/pmc_write \
+  --lds $O/r04b_step/pmc_lds --sq $O/r04b_step/pmc_sq --kernel "mapf_wave_kernel<5, false" --config c2_step --T 1 --E 4096 \
+  --tag r04_c2_step --command "python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --per-step-steps 200" \
+  --out $O/profiles/pmc_c2_step.json > /dev/null || exit 1
+python3 -c "
+import json
+for f in ('pmc_c3', 'pmc_c2_step'):
+    d = json.load(open('$O/profiles/%s.json' % f))
+    print(f, d['trace']['kernels'][0]['avg_ns'], d.get('traffic_bytes_per_launch'), (d.get('sq') or {}).get('wait_any_frac_of_wave_cycles'))
+"

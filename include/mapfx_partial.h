@@ -21,10 +21,10 @@
  * mode's random collision repair (:262-275) and the visualisation hooks.
  *
  * Limits: N <= 1024, H <= 1024, W <= 1536, and for a side above 256 the BFS
- * frontier rows must fit LDS: H * ceil(W / 64) * 8 <= 160 KB, i.e.
- * H * ceil(W / 64) <= 20480 (every map the reference ships fits: orz900d's 656 x 1491
- * needs 126 KB; a full 1024 x 1536 map would need 196 KB and is refused by
- * mapfx_partial_create).  N <= 64 with H, W <= 256 keeps each env in one wavefront
+ * frontier rows must fit LDS: H * ceil(W / 64) * 8 bytes plus the BFS kernel's few
+ * bytes of static LDS <= 160 KB, i.e. H * ceil(W / 64) just under 20480 (every map the
+ * reference ships fits: orz900d's 656 x 1491 needs 126 KB; a full 1024 x 1536 map
+ * would need 196 KB and is refused by mapfx_partial_create).  N <= 64 with H, W <= 256 keeps each env in one wavefront
  * with its cell maps in LDS; otherwise one workgroup steps an env with the agents'
  * cells in an LDS hash table and the obstacle bitmap read from HBM.
  */

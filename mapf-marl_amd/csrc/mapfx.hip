@@ -253,6 +253,15 @@ __device__ __forceinline__ __attribute__((unused)) uint32_t lds_addr(const void*
 #ifndef MAPFX_OCC_U
 #define MAPFX_OCC_U 1   // rows in flight per thread in write_occ16_rows (0: 4 at W <= 5, else 2)
 #endif
+#ifndef MAPFX_EDGE_READLANE
+#define MAPFX_EDGE_READLANE 1  // generic edge scan: the candidate's cells by v_readlane
+#endif
+#ifndef MAPFX_FOLD_PRIO
+#define MAPFX_FOLD_PRIO 3  // s_setprio of the deferred fold's chain (0: none)
+#endif
+#ifndef MAPFX_OCC_GROUPS
+#define MAPFX_OCC_GROUPS 1  // u16 occupancy windows as 8-row groups of 16-byte stores
+#endif
 #ifndef MAPFX_W0_WRITES
 #define MAPFX_W0_WRITES 1  // wave 0 writes window records on the steps without a fold
 #endif
@@ -365,7 +374,7 @@ __device__ void write_windows(const Geo& g, const unsigned char* lds, const int*
 // than the per-value writer above.
 template <int W>
 __device__ void write_occ16_rows(const Geo& g, const unsigned char* lds, const int* newc_blk,
-                                 unsigned char* dst, int nseg, int tid, int nt) {
+                                 unsigned char* dst, int nseg, int tid, int nt, int sg_begin = 0) {
   constexpr int NP = (W + 1) / 2;  // cell pairs per row (the last one half used)
   constexpr int h = W / 2;
   constexpr int U = MAPFX_OCC_U > 0 ? MAPFX_OCC_U : (W <= 5 ? 4 : 2);  // rows in flight per thread
@@ -374,7 +383,7 @@ __device__ void write_occ16_rows(const Geo& g, const unsigned char* lds, const i
   const bool one_env = g.EPB == 1;
   const uint32_t lbase = lds_addr(lds + g.off_map);
   const bool dalign = (((uintptr_t)dst) & 2u) == 0;
-  for (int sg0 = tid; sg0 < nseg; sg0 += U * nt) {
+  for (int sg0 = sg_begin + tid; sg0 < nseg; sg0 += U * nt) {
     int q[U], y[U];
     bool ok[U];
 #pragma unroll
@@ -422,6 +431,73 @@ __device__ void write_occ16_rows(const Geo& g, const unsigned char* lds, const i
       }
     }
   }
+}
+
+// obs_window_occ of u16 cells, odd window W <= 7, written as 16-byte stores: thread t
+// owns the 8 consecutive window rows 8t .. 8t + 7 of the block's record run (rows of
+// W int16: 8 rows = 16 W bytes = W whole 16-byte chunks, aligned when the run is).  Each
+// row is read once from the LDS map ((2W + 5) / 4 dwords realigned with v_alignbyte,
+// occ = count - obstacle two cells at a time as in write_occ16_rows), rows 2k and
+// 2k + 1 are spliced into W dwords (the odd row starts at a half dword: one v_perm and
+// alignbyte shifts), and the thread stores W dwordx4 -- against 3 stores (2 dwords +
+// one u16) per 10-byte row.  Returns the number of rows it covered (8 per whole group);
+// the caller writes the rest with write_occ16_rows.
+template <int W>
+__device__ int write_occ16_groups(const Geo& g, const unsigned char* lds, const int* newc_blk,
+                                  unsigned char* dst, int nseg, int tid, int nt) {
+  constexpr int NP = (W + 1) / 2;       // dwords of one row's occ values (the last half used)
+  constexpr int NR = (2 * W + 5) / 4;   // LDS dwords covering a row at either alignment
+  constexpr int h = W / 2;
+  typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  if ((((uintptr_t)dst) & 15u) != 0) return 0;
+  const int ngrp = nseg >> 3;
+  const int pitch = g.pitch;
+  const bool one_env = g.EPB == 1;
+  const uint32_t lbase = lds_addr(lds + g.off_map);
+  for (int grp = tid; grp < ngrp; grp += nt) {
+    const int sg0 = grp << 3;
+    int q = fastdiv(sg0, g.m_w);
+    int y = sg0 - q * W;
+    uint32_t out[4 * W];
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) {
+      uint32_t P[2][NP];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {  // rows 2 pr + j
+        const int slot = one_env ? 0 : fastdiv(q, g.m_N);
+        const int e0 = newc_blk[q] + (y - h) * pitch - h;  // first cell of the row
+        const uint32_t A = lbase + (uint32_t)(slot * g.map_env_bytes) + 2u * (uint32_t)e0;
+        lds_cu32* src = (lds_cu32*)(uintptr_t)(A & ~3u);
+        uint32_t Wd[NR + 1];
+#pragma unroll
+        for (int k = 0; k < NR; ++k) Wd[k] = src[k];
+        Wd[NR] = 0u;
+        const uint32_t sh = A & 2u;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+          const uint32_t c = __builtin_amdgcn_alignbyte(Wd[k + 1], Wd[k], sh);
+          P[j][k] = (((c & 0x7FFF7FFFu) | 0x80008000u) - ((c >> 15) & 0x00010001u)) ^ 0x80008000u;
+        }
+        if (++y == W) {
+          y = 0;
+          ++q;
+        }
+      }
+      // the pair's W dwords: row 2 pr's NP - 1 full dwords, its last value with the odd
+      // row's first, then the odd row's values 1 .. W - 1 shifted down by one u16
+      uint32_t* o = out + pr * W;
+#pragma unroll
+      for (int k = 0; k + 1 < NP; ++k) o[k] = P[0][k];
+      o[NP - 1] = __builtin_amdgcn_perm(P[1][0], P[0][NP - 1], 0x05040100u);
+#pragma unroll
+      for (int k = 0; k + 1 < NP; ++k) o[NP + k] = __builtin_amdgcn_alignbyte(P[1][k + 1], P[1][k], 2);
+    }
+    u32x4* d = (u32x4*)(dst + 16u * (uint32_t)W * (uint32_t)grp);
+#pragma unroll
+    for (int k = 0; k < W; ++k) d[k] = u32x4{out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]};
+  }
+  return ngrp << 3;
 }
 
 // ---------------------------------------------------------------------------
@@ -681,7 +757,9 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
           while (m) {
             const int src = __ffsll((unsigned long long)m) - 1;
             m &= m - 1;
-            const int tn = __shfl(nc[k], src), to = __shfl(oc[k], src);
+            // src is wave-uniform (a ballot bit): v_readlane, not two ds_bpermute round trips
+            const int tn = MAPFX_EDGE_READLANE ? __builtin_amdgcn_readlane(nc[k], src) : __shfl(nc[k], src);
+            const int to = MAPFX_EDGE_READLANE ? __builtin_amdgcn_readlane(oc[k], src) : __shfl(oc[k], src);
             int cnt = 0;
 #pragma unroll
             for (int q = 0; q < NCH; ++q)
@@ -793,6 +871,9 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     auto fold_ring = [&]() {
       const int s0 = s & ~(FR - 1);
       if (!env_ok || tid > s - s0 || (MAPFX_GABL & 1)) return;
+      // the fold is one dependent chain of N fp64 adds that competes for issue with the
+      // other blocks' window writers on its SIMD: it goes first while it runs
+      if (MAPFX_FOLD_PRIO) __builtin_amdgcn_s_setprio(MAPFX_FOLD_PRIO);
       const uint16_t* cs = codes + tid * (g.code_pitch >> 1);
       auto val = [&](uint32_t c) { return c < 32u ? ctab[c] : code_reward(g, c); };
       double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
@@ -835,6 +916,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       const long long ri = (long long)(s0 + tid) * Elong + env;
       if (a.reward) a.reward[ri] = R;
       if (a.reward_f32) a.reward_f32[ri] = (float)R;
+      if (MAPFX_FOLD_PRIO) __builtin_amdgcn_s_setprio(0);
     };
     // One env per block over four waves (N > 128): wave 0 runs the tail (the fold is
     // one dependent chain of N adds) while waves 1-3 write the window records; with
@@ -866,10 +948,19 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         if constexpr (sizeof(CellT) == 2) {
           const int nseg = nenv * N * g.window;
           done_occ = true;
-          if (g.window == 5) write_occ16_rows<5>(g, lds, newc_blk, dst, nseg, wtid, wnt);
-          else if (g.window == 3) write_occ16_rows<3>(g, lds, newc_blk, dst, nseg, wtid, wnt);
-          else if (g.window == 7) write_occ16_rows<7>(g, lds, newc_blk, dst, nseg, wtid, wnt);
-          else done_occ = false;
+          // whole 8-row groups as 16-byte stores, the remaining rows one by one
+          if (g.window == 5) {
+            const int rows = MAPFX_OCC_GROUPS ? write_occ16_groups<5>(g, lds, newc_blk, dst, nseg, wtid, wnt) : 0;
+            write_occ16_rows<5>(g, lds, newc_blk, dst, nseg, wtid, wnt, rows);
+          } else if (g.window == 3) {
+            const int rows = MAPFX_OCC_GROUPS ? write_occ16_groups<3>(g, lds, newc_blk, dst, nseg, wtid, wnt) : 0;
+            write_occ16_rows<3>(g, lds, newc_blk, dst, nseg, wtid, wnt, rows);
+          } else if (g.window == 7) {
+            const int rows = MAPFX_OCC_GROUPS ? write_occ16_groups<7>(g, lds, newc_blk, dst, nseg, wtid, wnt) : 0;
+            write_occ16_rows<7>(g, lds, newc_blk, dst, nseg, wtid, wnt, rows);
+          } else {
+            done_occ = false;
+          }
         }
         if (!done_occ)
           write_windows<CellT, true>(g, lds, newc_blk, dst, nenv * N * (wlen / 2), wtid, wnt);

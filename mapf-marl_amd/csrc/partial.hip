@@ -1369,13 +1369,21 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
     delete h;
     return perr(MAPFX_EINVAL, "one env needs more than 160 KB of LDS (map too large)");
   }
-  if (g.big && g.huge_lds > 160 * 1024) {
-    char msg[200];
-    snprintf(msg, sizeof msg,
-             "MARL_PARTIAL: the %d x %d map's BFS frontier needs H * ceil(W / 64) * 8 = %d B of "
-             "LDS (> 160 KB: H * ceil(W / 64) must be <= 20480)", c.H, c.W, g.huge_lds);
-    delete h;
-    return perr(MAPFX_EINVAL, msg);
+  if (g.big && g.huge_lds > 0) {
+    // the frontier rows plus the kernel's own static LDS (__syncthreads_or's scratch)
+    hipFuncAttributes fa;
+    memset(&fa, 0, sizeof fa);
+    (void)hipFuncGetAttributes(&fa, g.gd32 ? (const void*)partial_bfs_huge_kernel<int32_t>
+                                           : (const void*)partial_bfs_huge_kernel<int16_t>);
+    if (g.huge_lds + (int)fa.sharedSizeBytes > 160 * 1024) {
+      char msg[240];
+      snprintf(msg, sizeof msg,
+               "MARL_PARTIAL: the %d x %d map's BFS frontier needs H * ceil(W / 64) * 8 = %d B of "
+               "LDS (+ %d B static; the CU has 160 KB: H * ceil(W / 64) must stay below ~20470)",
+               c.H, c.W, g.huge_lds, (int)fa.sharedSizeBytes);
+      delete h;
+      return perr(MAPFX_EINVAL, msg);
+    }
   }
   if (g.big && g.wg_lds > 160 * 1024) {
     delete h;
@@ -1415,11 +1423,17 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
       rc0 = check_hip(hipFuncSetAttribute((const void*)pick_wg(g.win, wg_apl(g)),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, g.wg_lds),
                       "hipFuncSetAttribute(partial_wg_kernel LDS)");
-    if (!rc0 && g.huge_lds > 64 * 1024)
-      rc0 = check_hip(hipFuncSetAttribute(g.gd32 ? (const void*)partial_bfs_huge_kernel<int32_t>
-                                                 : (const void*)partial_bfs_huge_kernel<int16_t>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, g.huge_lds),
-                      "hipFuncSetAttribute(partial_bfs_huge_kernel LDS)");
+    if (!rc0 && g.huge_lds > 64 * 1024 &&
+        hipFuncSetAttribute(g.gd32 ? (const void*)partial_bfs_huge_kernel<int32_t>
+                                   : (const void*)partial_bfs_huge_kernel<int16_t>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, g.huge_lds) != hipSuccess) {
+      (void)hipGetLastError();
+      char msg[200];
+      snprintf(msg, sizeof msg,
+               "MARL_PARTIAL: the %d x %d map's BFS frontier (H * ceil(W / 64) * 8 = %d B) exceeds "
+               "the LDS a workgroup may allocate", c.H, c.W, g.huge_lds);
+      rc0 = perr(MAPFX_EINVAL, msg);
+    }
     if (rc0) {
       delete h;
       return rc0;

@@ -128,11 +128,14 @@ def test_partial_wg_path_matches_oracle(mapfx_mod, S, N, E, T, win, K):
 
 def test_partial_refuses_frontier_past_lds(mapfx_mod):
     """A side above 256 keeps the BFS frontier rows in LDS: H * ceil(W / 64) * 8 B must
-    fit 160 KB (include/mapfx_partial.h).  1024 x 1536 needs 196 KB and is refused with
-    that reason; 853 x 1536 (the largest height at that width) is accepted."""
+    fit 160 KB with the kernel's static LDS (include/mapfx_partial.h).  1024 x 1536 needs
+    196 KB and is refused with that reason, as is 853 x 1536 (159.9 KB + the static
+    bytes); 840 x 1536 (157.5 KB) is accepted."""
     kw = dict(obs_window=5, obs_knn_agents=3, episode_limit=10)
     ip = np.array([[[0, 0], [0, 1]]], np.int32)
     gl = np.array([[[1, 0], [1, 1]]], np.int32)
     with pytest.raises(mapfx_mod.MapfxError, match="BFS frontier"):
         mapfx_mod.MarlPartialBatch(ip, gl, grids=np.zeros((1, 1024, 1536), np.int8), **kw)
-    mapfx_mod.MarlPartialBatch(ip, gl, grids=np.zeros((1, 853, 1536), np.int8), **kw)
+    with pytest.raises(mapfx_mod.MapfxError, match="BFS frontier"):
+        mapfx_mod.MarlPartialBatch(ip, gl, grids=np.zeros((1, 853, 1536), np.int8), **kw)
+    mapfx_mod.MarlPartialBatch(ip, gl, grids=np.zeros((1, 840, 1536), np.int8), **kw)

@@ -1503,6 +1503,15 @@ __device__ __forceinline__ void stage_occ_record(const uint32_t (&R)[(WIN * WIN 
 #ifndef MAPFX_SPLIT_WAVES
 #define MAPFX_SPLIT_WAVES (MAPFX_SPLIT_MOVE ? 4 : MAPFX_SPLIT_ALT ? 3 : 2)  // 3 without ALT: record wave + small-output wave
 #endif
+#ifndef MAPFX_SPLIT_LAG
+// 1 (ALT only): the step images are a 3-slot ring published one barrier late.  The step
+// wave writes step q's image in iteration q + 1 and the store waves read it after barrier
+// q + 3, so the step wave's barrier waits for everything but its own latest image writes
+// (s_waitcnt lgkmcnt(NQ)): the image stores of a step leave its critical path (round 4,
+// C2: cutting them to one store per lane measured -1.4 us per T = 20 launch).
+#define MAPFX_SPLIT_LAG (MAPFX_SPLIT_ALT && !MAPFX_SPLIT_MOVE)
+#endif
+constexpr int SPLIT_NIMG = MAPFX_SPLIT_LAG ? 3 : 2;  // step images in the ring
 // step-side waves ahead of the store waves
 #define MAPFX_SPLIT_SW0 (MAPFX_SPLIT_MOVE ? 2 : 1)
 constexpr int SPLIT_RING_LDS = 2 * 64 * 16;  // MOVE -> MAP ring: 2 steps x 64 lanes x u32x4
@@ -1550,6 +1559,17 @@ constexpr uint32_t SF_DONE = 1, SF_LIVE = 2, SF_DNOLD = 4, SF_ENVC = 8, SF_SKIP 
 __device__ __forceinline__ void split_barrier() {
   if (MAPFX_ABLATE & 1024) return;  // diagnostic only: no hand-over (results are garbage)
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// The step wave's barrier under MAPFX_SPLIT_LAG: every LDS operation but the NQ most
+// recent (this iteration's image stores, which nobody reads before the NEXT barrier) has
+// completed.  LDS operations of a wave complete in order, and an iteration issues more
+// than NQ of them after the previous iteration's image stores, so those are complete;
+// an outstanding scalar load only makes the wait stricter.
+template <int NQ>
+__device__ __forceinline__ void split_barrier_lag() {
+  static_assert(NQ >= 0 && NQ < 16, "lgkmcnt");
+  if (MAPFX_ABLATE & 1024) return;
+  asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" ::"n"(NQ) : "memory");
 }
 
 template <typename P, typename V>
@@ -1680,7 +1700,11 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
     if ((q & 15u) == 15u || q + 1 == (uint32_t)T) fold_batch(q & ~15u, (int)(q & 15u) + 1);
   };
 
-  const int rounds = T > 0 ? T + 1 : 0;
+  // MAPFX_SPLIT_LAG: step q's image is complete at barrier q + 3 (ring slot q % 3), one
+  // barrier later than without it (barrier q + 2, buffer (q + 1) & 1)
+  constexpr int LAGS = MAPFX_SPLIT_LAG ? 1 : 0;
+  const int rounds = T > 0 ? T + 1 + LAGS : 0;
+  int islot = 0;  // LAG: ring slot of the image read next
   for (int s = 1; s <= rounds; ++s) {
 #ifdef MAPFX_STAMPS  // diagnostic: end of round s - 1's work (columns 5 / 7 of row s - 1)
     if (s > 1) {
@@ -1690,11 +1714,13 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
     }
 #endif
     split_barrier();
-    if (s == 1 || (MAPFX_ABLATE & 256)) continue;
-    const int q = s - 2;
+    if (s <= 1 + LAGS || (MAPFX_ABLATE & 256)) continue;
+    const int q = s - 2 - LAGS;
+    const int qslot = MAPFX_SPLIT_LAG ? islot : ((s - 1) & 1);
+    if (MAPFX_SPLIT_LAG) islot = islot == SPLIT_NIMG - 1 ? 0 : islot + 1;
     if ((q & 1) == par) {  // a(q)
       const u32x4* sl = (const u32x4*)__builtin_assume_aligned(
-          sp + ((s - 1) & 1) * g.wv_split_buf + lane * SLOT_LANE, 16);
+          sp + qslot * g.wv_split_buf + lane * SLOT_LANE, 16);
       uint32_t w[4 * NQ];
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
@@ -1931,7 +1957,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
       }
       split_barrier();
       unsigned char* sp = lds + g.wv_off_split;
-      unsigned char* own = sp + 2 * g.wv_split_buf;
+      unsigned char* own = sp + SPLIT_NIMG * g.wv_split_buf;
       constexpr int RECB = OCC ? WIN * WIN : 2 * WIN * WIN;  // one wave's staged image: 64 * RECB
       double* rtab = (double*)(own + 2 * 64 * RECB);          // ALT: reward table + code ring
       const int par = (int)(threadIdx.x >> 6) - MAPFX_SPLIT_SW0;  // ALT: this wave's step parity
@@ -2162,14 +2188,17 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
     return edge;
   };
 
+  int hslot = 0;  // SPLIT + MAPFX_SPLIT_LAG: ring slot of the next step image
   // HEAVY part of step q (slot qs): window, node, edge, reward, per-agent stores.
   auto heavy = [&](int qs) {
     if constexpr (SPLIT) {  // step q's info word and raw window rows -> image (qs + 1) & 1
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
       using SL = SplitLayout<WIN, LL>;
       const int edge = edge_of();
+      const int hs = MAPFX_SPLIT_LAG ? hslot : ((qs + 1) & 1);  // LAG: ring slot qs % 3
+      if (MAPFX_SPLIT_LAG) hslot = hslot == SPLIT_NIMG - 1 ? 0 : hslot + 1;
       u32x4* sl = (u32x4*)__builtin_assume_aligned(
-          lds + g.wv_off_split + ((qs + 1) & 1) * g.wv_split_buf + lane64 * SLOT_LANE, 16);
+          lds + g.wv_off_split + hs * g.wv_split_buf + lane64 * SLOT_LANE, 16);
       const uint32_t fl = (q_dn ? SF_DONE : 0u) | (q_live ? SF_LIVE : 0u) | (q_dnold ? SF_DNOLD : 0u) |
                           (q_envc ? SF_ENVC : 0u) | (q_skip ? SF_SKIP : 0u) |
                           (q_alldone ? SF_ALLDONE : 0u) | ((uint32_t)(edge > 255 ? 255 : edge) << 8);
@@ -2313,7 +2342,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     constexpr int RECB = OCC ? WIN * WIN : 2 * WIN * WIN;
     u32x4* ring = (u32x4*)__builtin_assume_aligned(
-        lds + g.wv_off_split + 2 * g.wv_split_buf + 2 * 64 * RECB + SPLIT_FOLD_LDS, 16);
+        lds + g.wv_off_split + SPLIT_NIMG * g.wv_split_buf + 2 * 64 * RECB + SPLIT_FOLD_LDS, 16);
     if (is_map) {
       if (!fast) {  // the one-wave step side runs on wave 0: only its barriers
         for (int s = 1; s <= T + 1; ++s) split_barrier();
@@ -2568,8 +2597,12 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
       }
     }
     STAMP(4);
-    if constexpr (SPLIT) split_barrier();  // image s & 1 -> store wave
-    else wave_fence();
+    if constexpr (SPLIT) {  // image s & 1 (LAG: the previous iteration's image) -> store waves
+      if constexpr (MAPFX_SPLIT_LAG && WIN > 0) split_barrier_lag<SplitLayout<WIN, LL>::SLOT / 16>();
+      else split_barrier();
+    } else {
+      wave_fence();
+    }
     STAMP(6);
   }
 #ifdef MAPFX_CLOCKS
@@ -2588,7 +2621,8 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
   // ---- drain the pipeline: heavy part of the last step, the last two tails ----
   if (SPLIT && T > 0) {
     heavy(T - 1);
-    split_barrier();  // image T & 1: the last step
+    if constexpr (SPLIT && MAPFX_SPLIT_LAG && WIN > 0) split_barrier_lag<SplitLayout<WIN, LL>::SLOT / 16>();
+    split_barrier();  // image T & 1 (LAG: ring slot (T - 1) % 3): the last step
   } else if (T > 0) {
     const double Rp = (ROLL && T > 1) ? fold(T & 1) : 0.0;  // step T-2's row
     heavy(T - 1);
@@ -2782,7 +2816,7 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
                            (uintptr_t)a.traj_done | (uintptr_t)a.reward | (uintptr_t)a.traj_t;
     // + staged-record images of the store wave (2 x 64 records)
     // (+ ALT: the 256-entry reward table and the 32-step code ring)
-    const int split_lds = g.wv_lds + 2 * g.wv_split_buf + 2 * 64 * (occ ? g.wlen / 2 : g.wlen) +
+    const int split_lds = g.wv_lds + SPLIT_NIMG * g.wv_split_buf + 2 * 64 * (occ ? g.wlen / 2 : g.wlen) +
                           (MAPFX_SPLIT_ALT ? SPLIT_FOLD_LDS : 0) + (MAPFX_SPLIT_MOVE ? SPLIT_RING_LDS : 0);
     const bool split = MAPFX_SPLIT && runner && fullw && g.L == 16 && g.wv_split_buf > 0 &&
                        split_lds <= 64 * 1024 && (al16 & 15) == 0;

@@ -21,3 +21,11 @@ for f in ('pmc_c3', 'pmc_c2_step'):
     d = json.load(open('$O/profiles/%s.json' % f))
     print(f, d['trace']['kernels'][0]['avg_ns'], d.get('traffic_bytes_per_launch'), (d.get('sq') or {}).get('wait_any_frac_of_wave_cycles'))
 "
+# the runner's per-step kernels (where its ~66 us per step go)
+mkdir -p $O/r04b_runner
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/r04b_runner/trace -o run --output-format csv \
+  -- python3 bench.py --env runner --cpu-seconds 0 --steps 200 --warmup 100 > $O/r04b_runner/bench.json 2> $O/r04b_runner/err.txt || exit 1
+tail -c 300 $O/r04b_runner/bench.json; echo
+# MARL_PARTIAL: this round's kernel vs round 3's (carried goal distance, early lookups)
+mkdir -p $O/r04b_runner; bash tools/ab_bench.sh $O/r04b_pab 2 "--env marl_partial" mapf-marl_amd/mapfx/libmapfx.so \
+  mapf-marl_amd/mapfx/libmapfx_oldpartial.so || true

@@ -63,7 +63,11 @@ typedef struct mapfx_runner_state {
   double* ep_return;     /* [B] episode_returns (:139, fp64 like the Python floats)  */
   int64_t* ep_length;    /* [B] episode_lengths (:140)                              */
   int64_t* env_steps;    /* [1] env_steps_this_run (:142)                           */
-  int8_t* env_actions;   /* [B][N] the actions the env step reads                   */
+  int8_t* env_actions;   /* [B][N] the actions the env step reads (mapfx_runner_actions) */
+  int32_t* bs_inv;       /* [B] row of env b in bs, -1 when b is not in it: the fused
+                            step (mapfx_runner_step) reads env b's actions from row
+                            bs_inv[b] of the MAC's output and writes its actions rows
+                            there, so no separate actions pass runs (appended in ABI 3) */
 } mapfx_runner_state;
 
 /* reset(): every env's observations (from `out` of mapfx_partial_reset) into row
@@ -88,11 +92,14 @@ int mapfx_runner_post(const mapfx_runner_state* rs, const uint8_t* terminated,
                       const mapfx_partial_out* out, int32_t ts, int32_t* counts_out,
                       const mapfx_episode_rows* rows, void* stream);
 
-/* One runner step in one call: mapfx_runner_actions, the env step of
- * mapfx_partial_step(h, st, rs->env_actions, MAPFX_I8, out) and mapfx_runner_post(rs,
- * st->terminated, out, ...).  When rows->obs is set, the env step writes the
- * observation rows of the envs running before it straight into rows->obs at ts + 1
- * (out->obs is then not written) and the post kernel copies no observation bytes. */
+/* One runner step in one call: the env step of mapfx_partial_step with every env's
+ * actions read from row bs_inv[b] of `actions` (stay for an env not in bs: it is no
+ * longer running and nothing of it is recorded), which also writes the actions /
+ * actions_onehot rows at ts of the envs in bs -- what mapfx_runner_actions does, in the
+ * same launch -- then mapfx_runner_post(rs, st->terminated, out, ...).  When rows->obs
+ * is set, the env step writes the observation rows of the envs running before it
+ * straight into rows->obs at ts + 1 (out->obs is then not written) and the post kernel
+ * copies no observation bytes. */
 int mapfx_runner_step(mapfx_partial_t* h, const mapfx_partial_state* st, const mapfx_partial_out* out,
                       const mapfx_runner_state* rs, const void* actions, int32_t action_dtype,
                       int64_t row_stride, int32_t ts, int32_t* counts_out,

@@ -39,6 +39,28 @@
 #define PABL 0  // diagnostic builds only: 1 skip the obs rows, 2 skip the step, 4 skip the staged copy
 #endif
 
+#ifdef PARTIAL_STAMPS
+// Diagnostic build only (never the shipped library): s_memtime stamps of partial_kernel's
+// phases, block 0 / lane 0, read back with mapfx_partial_debug_stamps().
+__device__ unsigned long long g_pstamps[16];
+#define PST(k)                                                                   \
+  do {                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    unsigned long long t_;                                                       \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                           \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_pstamps[(k)] = t_;                \
+  } while (0)
+extern "C" int mapfx_partial_debug_stamps(unsigned long long* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_pstamps), sizeof(unsigned long long) * 16) ==
+                 hipSuccess ? 0 : -1;
+}
+#else
+#define PST(k) \
+  do {         \
+  } while (0)
+#endif
+
 namespace {
 
 constexpr int NF = 13;   // KNN features per agent (:81)
@@ -95,6 +117,8 @@ struct PArgs {
   float* obs_rows;
   long long obs_env_stride;
   const uint8_t* obs_mask;
+  // the runner's fused actions (mapfx_partial_step_runner; act_row NULL otherwise)
+  mapfx_runner_acts ra;
 };
 
 // where env e's observation rows go ([N][D] floats), or nullptr when not written
@@ -108,6 +132,30 @@ __device__ inline int load_act(const void* p, int dtype, long long idx) {
   if (dtype == MAPFX_I32) return ((const int32_t*)p)[idx];
   const long long v = ((const int64_t*)p)[idx];
   return (v < -1 || v > 5) ? -1 : (int)v;
+}
+
+// The step's action of agent `ag` of env `env` (oa = env * N + ag).  The runner's fused
+// form (a.ra.act_row): row act_row[env] of the MAC's output, recorded into the
+// EpisodeBatch's actions / actions_onehot rows at ts (parallel_runner.py:104-110 and the
+// OneHot preprocess); an env outside bs stays (it has terminated: nothing of it is
+// recorded again).  Values outside 0..4 come back as -1 (the env is then skipped, :174).
+__device__ inline int step_action(const PArgs& a, int env, int ag, long long oa) {
+  if (!a.ra.act_row) return load_act(a.actions, a.act_dtype, oa);
+  const int row = a.ra.act_row[env];
+  if (row < 0) return 4;
+  const long long i = (long long)row * a.ra.act_row_stride + ag;
+  const long long v = a.act_dtype == MAPFX_I8 ? (long long)((const int8_t*)a.actions)[i]
+                      : a.act_dtype == MAPFX_I32 ? (long long)((const int32_t*)a.actions)[i]
+                                                 : ((const int64_t*)a.actions)[i];
+  if (a.ra.ep_actions)
+    a.ra.ep_actions[(long long)env * a.ra.ep_actions_sb + (long long)a.ra.ts * a.ra.ep_actions_st + ag] = v;
+  if (a.ra.ep_onehot) {
+    float* oh = a.ra.ep_onehot + (long long)env * a.ra.ep_onehot_sb + (long long)a.ra.ts * a.ra.ep_onehot_st +
+                (long long)ag * 5;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) oh[k] = v == k ? 1.0f : 0.0f;
+  }
+  return (v < 0 || v > 4) ? -1 : (int)v;
 }
 
 __device__ inline void wave_fence() {
@@ -492,7 +540,7 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
   for (int k = 0; k < APL; ++k) {
     act[k] = 4;
     if (a.do_step && has[k]) {
-      act[k] = load_act(a.actions, a.act_dtype, (long long)env * N + tid + k * WG_THREADS);
+      act[k] = step_action(a, env, tid + k * WG_THREADS, (long long)env * N + tid + k * WG_THREADS);
       if (act[k] < 0 || act[k] > 4) bad = true;
     }
   }
@@ -750,6 +798,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   int2* posL = (int2*)(lds + g.off_pos + cs * (64 * 8));
   double* rewL = (double*)(lds + g.off_rew + cs * g.rew_env_bytes);
 
+  PST(0);
   const long long oa = (long long)env * N + ag;
   // ---- state ----
   int r = 0, c = 0, gr = 0, gc = 0, ir = 0, ic = 0, steps = 0, gcost = -1, edge = 0;
@@ -791,7 +840,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   // the step's action, loaded with the state (its lookup below needs it)
   int act = 4;
   if (a.do_step && has) {
-    act = load_act(a.actions, a.act_dtype, oa);
+    act = step_action(a, env, ag, oa);
     if (act < 0 || act > 4) act = -1;
   }
   if (reset_me) {
@@ -807,6 +856,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   // goal-path distances (:227-233): the move target's entry, speculatively (used when the
   // agent moves), and the current cell's when no carried value applies -- issued here, so
   // their latency overlaps the map build
+  PST(1);
   const bool need_cur = has && (!a.do_step || !a.pdist || pd == PD_NONE);
   int npd_t = 0;
   if (has) {
@@ -841,6 +891,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   if (has) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
   wave_fence();
 
+  PST(2);
   // ---- step (:165-310) ----
   if (a.do_step && env_ok && !(PABL & 2)) {
     const bool skip = (__ballot(act < 0) & envmask) != 0;  // the reference asserts (:174)
@@ -936,6 +987,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   }
   wave_fence();
 
+  PST(3);
   // ---- observations of the current state (:312-391) ----
   // per-agent feature rows: curr, start, goal, unit vec, norm, node, edge, steps
   if (has) {
@@ -950,6 +1002,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
     posL[ag] = make_int2(r, c);
   }
   wave_fence();
+  PST(4);
   constexpr int WW = WIN * WIN;
   constexpr int DF = (KF > 0 && LF > 0) ? 2 * WW + NF * KF : 1;  // fast-path row length
   float o[DF];
@@ -1068,6 +1121,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
     }
     (void)kn;
   }
+  PST(5);
   if constexpr (KF > 0 && LF > 0) {
     // The rows of the envs of a staging group (the whole wave, or each half of it) are
     // one contiguous run of the destination (a.obs), or one run per env (EpisodeBatch
@@ -1143,6 +1197,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
       }
     }
   }
+  PST(6);
   (void)o;
   // avail (:399-433): neighbour in bounds and not a free-standing obstacle
   if (has && a.avail) {
@@ -1177,6 +1232,11 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
     a.terminated[env] = term ? 1 : 0;
     a.total_coll[env] = total;
   }
+  PST(7);
+#ifdef PARTIAL_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  PST(8);
+#endif
 }
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -1582,6 +1642,32 @@ int mapfx_partial_step_rows(mapfx_partial_t* h, const mapfx_partial_state* st, c
   a.obs_mask = obs_mask;
   a.actions = actions;
   a.act_dtype = action_dtype;
+  a.do_step = 1;
+  return launch(h, a, stream);
+}
+
+int mapfx_partial_step_runner(mapfx_partial_t* h, const mapfx_partial_state* st, const void* actions,
+                              int action_dtype, const mapfx_runner_acts* ra, const mapfx_partial_out* out,
+                              float* obs_rows, long long obs_env_stride, const uint8_t* obs_mask,
+                              void* stream) {
+  if (!h) return perr(MAPFX_EINVAL, "NULL handle");
+  int rc = check_state(h, st);
+  if (rc) return rc;
+  if (!actions || !ra || !ra->act_row) return perr(MAPFX_EINVAL, "NULL actions / rows map");
+  if (action_dtype < MAPFX_I8 || action_dtype > MAPFX_I64) return perr(MAPFX_EINVAL, "bad action_dtype");
+  PArgs a;
+  memset(&a, 0, sizeof(a));
+  fill_state(a, st);
+  fill_out(a, out);
+  if (obs_rows) {
+    a.obs = nullptr;
+    a.obs_rows = obs_rows;
+    a.obs_env_stride = obs_env_stride;
+    a.obs_mask = obs_mask;
+  }
+  a.actions = actions;
+  a.act_dtype = action_dtype;
+  a.ra = *ra;
   a.do_step = 1;
   return launch(h, a, stream);
 }

@@ -73,6 +73,7 @@ __global__ void __launch_bounds__(RB) runner_begin_kernel(mapfx_runner_state rs,
     rs.alive[b] = 1;
     rs.alive_prev[b] = 1;
     rs.bs[b] = b;
+    if (rs.bs_inv) rs.bs_inv[b] = b;
     rs.ep_return[b] = 0.0;
     rs.ep_length[b] = 0;
     if (b == 0) {
@@ -171,8 +172,11 @@ __global__ void __launch_bounds__(CT) runner_compact_kernel(mapfx_runner_state r
     total_a += wsum_a[i];
   }
   int o = off + x - c;  // exclusive prefix of this thread's chunk
-  for (int b = lo; b < hi; ++b)
-    if (rs.alive_prev[b]) rs.bs[o++] = b;
+  for (int b = lo; b < hi; ++b) {
+    const bool in = rs.alive_prev[b] != 0;
+    if (rs.bs_inv) rs.bs_inv[b] = in ? o : -1;  // where the next MAC call puts env b's row
+    if (in) rs.bs[o++] = b;
+  }
   __syncthreads();  // bs[0] written
   const int64_t first = total > 0 ? rs.bs[0] : 0;
   for (int j = total + threadIdx.x; j < rs.B; j += CT) rs.bs[j] = first;
@@ -244,18 +248,35 @@ int mapfx_runner_step(mapfx_partial_t* h, const mapfx_partial_state* st, const m
                       const mapfx_runner_state* rs, const void* actions, int32_t action_dtype,
                       int64_t row_stride, int32_t ts, int32_t* counts_out,
                       const mapfx_episode_rows* rows, void* stream) {
-  int rc = mapfx_runner_actions(rs, actions, action_dtype, row_stride, ts, rows, stream);
+  int rc = check_rs(rs);
   if (rc) return rc;
-  if (!rows || !rows->obs)
-    return (rc = mapfx_partial_step(h, st, rs->env_actions, MAPFX_I8, out, stream))
+  if (!rows) return err(MAPFX_EINVAL, "runner_step: NULL rows");
+  if (ts < 0 || ts >= rows->max_t) return err(MAPFX_EINVAL, "runner_step: ts outside the batch");
+  if (!rs->bs_inv)  // the unfused form: a separate actions pass into env_actions
+    return (rc = mapfx_runner_actions(rs, actions, action_dtype, row_stride, ts, rows, stream)) ? rc
+           : (rc = mapfx_partial_step(h, st, rs->env_actions, MAPFX_I8, out, stream))
                ? rc : mapfx_runner_post(rs, st->terminated, out, ts, counts_out, rows, stream);
-  // fused: the env step writes the observation rows of the envs running before it
-  // (rs->alive, updated only by the post kernel) straight into the batch's time row
-  // ts + 1, so the post kernel moves no observation bytes
-  float* obs_row = ts + 1 < rows->max_t ? rows->obs + (int64_t)(ts + 1) * rows->obs_st : nullptr;
-  if ((rc = mapfx_partial_step_rows(h, st, rs->env_actions, MAPFX_I8, out, obs_row, rows->obs_sb,
-                                    rs->alive, stream)))
+  // the env step reads each env's actions from the MAC's output (row bs_inv[b]) and
+  // writes the actions / one-hot rows at ts itself; when the batch has observation rows
+  // it also writes those of the envs running before it (rs->alive, updated only by the
+  // post kernel) straight into time row ts + 1, so the post kernel moves no observation
+  // bytes
+  mapfx_runner_acts ra;
+  memset(&ra, 0, sizeof ra);
+  ra.act_row = rs->bs_inv;
+  ra.act_row_stride = row_stride;
+  ra.ep_actions = rows->actions;
+  ra.ep_actions_sb = rows->actions_sb;
+  ra.ep_actions_st = rows->actions_st;
+  ra.ep_onehot = rows->onehot;
+  ra.ep_onehot_sb = rows->onehot_sb;
+  ra.ep_onehot_st = rows->onehot_st;
+  ra.ts = ts;
+  float* obs_row = rows->obs && ts + 1 < rows->max_t ? rows->obs + (int64_t)(ts + 1) * rows->obs_st : nullptr;
+  if ((rc = mapfx_partial_step_runner(h, st, actions, action_dtype, &ra, out, obs_row, rows->obs_sb,
+                                      rs->alive, stream)))
     return rc;
+  if (!rows->obs) return mapfx_runner_post(rs, st->terminated, out, ts, counts_out, rows, stream);
   mapfx_episode_rows r2 = *rows;
   r2.obs = nullptr;
   return mapfx_runner_post(rs, st->terminated, out, ts, counts_out, &r2, stream);

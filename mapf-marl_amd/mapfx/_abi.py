@@ -108,7 +108,7 @@ class ERows(ctypes.Structure):  # include/mapfx_runner.h mapfx_episode_rows
 class RState(ctypes.Structure):  # include/mapfx_runner.h mapfx_runner_state
     _fields_ = [("B", c_i32), ("N", c_i32), ("D", c_i32)] + [
         (k, c_vp) for k in ("alive", "alive_prev", "bs", "counts", "ep_return", "ep_length",
-                            "env_steps", "env_actions")]
+                            "env_steps", "env_actions", "bs_inv")]
 
 
 ABI_VERSION = 3  # include/mapfx.h MAPFX_ABI_VERSION

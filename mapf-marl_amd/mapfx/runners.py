@@ -120,11 +120,13 @@ class ParallelRunner:
         self._ep_return, self._ep_length = z((B,), torch.float64), z((B,), torch.int64)
         self._env_steps = z((1,), torch.int64)
         self._env_actions = torch.full((B, N), 4, dtype=torch.int8, device=dev)
+        # row of env b in bs (-1: not in it): the fused step reads b's actions there
+        self._bs_inv = torch.full((B,), -1, dtype=torch.int32, device=dev)
         self._rs = _abi.RState(B=B, N=N, D=self.env.obs_dim, alive=ptr(self._alive),
                                alive_prev=ptr(self._alive_prev), bs=ptr(self._bs),
                                counts=ptr(self._counts), ep_return=ptr(self._ep_return),
                                ep_length=ptr(self._ep_length), env_steps=ptr(self._env_steps),
-                               env_actions=ptr(self._env_actions))
+                               env_actions=ptr(self._env_actions), bs_inv=ptr(self._bs_inv))
         # counts {len(bs), running} of step k land in slot k % _RING of a mapped host
         # buffer, written by the compaction kernel itself (no copy launch); the slot's
         # event marks them final

@@ -8,8 +8,8 @@ mkdir -p "$OUT"
 for r in $(seq 1 "$R"); do
   for lib in "$@"; do
     tag=$(basename "$lib" .so)
-    MAPFX_LIB=$PWD/$lib timeout -k 10 200 python3 bench.py $ARGS --cpu-seconds 0 --per-step-steps 0 \
+    MAPFX_LIB=$PWD/$lib timeout -k 10 200 python3 bench.py --per-step-steps 0 $ARGS --cpu-seconds 0 \
       > "$OUT/$tag.r$r.json" 2> "$OUT/$tag.r$r.err" || { tail -20 "$OUT/$tag.r$r.err"; exit 1; }
-    python3 -c "import json,sys; d=json.load(open('$OUT/$tag.r$r.json')); k=d.get('kernel_ms_per_launch', d.get('kernel_ms_per_step')); print('%-22s r$r %.5f' % ('$tag', k), (d.get('timing') or {}).get('kernel_ms_replays'), d['roofline']['frac'])"
+    python3 -c "import json,sys; d=json.load(open('$OUT/$tag.r$r.json')); k=d.get('kernel_ms_per_launch', d.get('kernel_ms_per_step')); print('%-22s r$r %.5f' % ('$tag', k), (d.get('timing') or {}).get('kernel_ms_replays'), d['roofline']['frac'], 'per_step', (d.get('per_step') or {}).get('kernel_ms'))"
   done
 done

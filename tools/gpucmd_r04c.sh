@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r04c
 mkdir -p $OUT
 L=mapf-marl_amd/mapfx
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dist.py -x -q --timeout 300 \
+timeout -k 10 800 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dist.py tests/test_gpu_runner.py tests/test_gpu_partial.py tests/test_partial_output_mode.py -x -q --timeout 300 \
   --timeout-method thread > $OUT/tests.txt 2>&1 || { grep -E "FAIL|Error" $OUT/tests.txt | head -30; tail -30 $OUT/tests.txt; exit 1; }
 tail -1 $OUT/tests.txt
 bash tools/ab_bench.sh $OUT/ab20 3 "--gpus 1 --steps 20 --warmup 5" $L/libmapfx.so $L/libmapfx_nolag.so || exit 1

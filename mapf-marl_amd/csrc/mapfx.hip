@@ -259,6 +259,12 @@ __device__ __forceinline__ __attribute__((unused)) uint32_t lds_addr(const void*
 #ifndef MAPFX_FOLD_PRIO
 #define MAPFX_FOLD_PRIO 3  // s_setprio of the deferred fold's chain (0: none)
 #endif
+#ifndef MAPFX_GEN_CARRY
+// 1: generic rollouts carry each agent's 4 neighbour cells (blocked / occupied bits) from
+// the post-step map of one step to the move decision of the next, and raise an invalid
+// next action's flag one step early, so a step needs no pre-step map read and no B1
+#define MAPFX_GEN_CARRY 1
+#endif
 #ifndef MAPFX_OCC_GROUPS
 #define MAPFX_OCC_GROUPS 1  // u16 occupancy windows as 8-row groups of 16-byte stores
 #endif
@@ -571,7 +577,10 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   int* rcs = (int*)(lds + g.off_rc) + slot * N;
   int* gls = (int*)(lds + g.off_goal) + slot * N;
   double* rew = (double*)(lds + g.off_rew) + slot * N;  // aliases bitsL (used after the build)
-  int* flag = (int*)(lds + g.off_flag) + slot * 8;  // [parity*4 + {alldone, bad}]
+  // [slot * 4 + {alldone, bad}]: two slots by step parity, three with MAPFX_GEN_CARRY (the
+  // next step's bad-action flag is raised during this step)
+  int* flag = (int*)(lds + g.off_flag) + slot * 12;
+  constexpr bool CARRY = ROLL && MAPFX_GEN_CARRY != 0;
   // Deferred fold (rollouts, one env per block): every step stores a u16 reward CODE
   // per agent in a ring of FR rows (aliasing rew / the bitmap); every FR-th step (and
   // the last) lanes 0..FR-1 of wave 0 fold one row each -- the same agent-order chain
@@ -606,13 +615,22 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   }
   int tcur = env_ok ? a.t[env] : 0;
 
+  const int T = ROLL ? a.T : 1;
+  // actions are loaded one step ahead: step s + 1's load is issued before step s's
+  // stores, so waiting for it never waits for them (vmcnt counts both, in order)
+  const bool read_act = a.do_step && !a.use_rng;
+  int act_nx[APL];
+#pragma unroll
+  for (int k = 0; k < APL; ++k)
+    act_nx[k] = (has[k] && read_act)
+                    ? load_action(a.actions, a.act_dtype, (long long)env * N + lane + k * g.L) : 4;
   // ---- stage the bitmap, build the padded map, add the agents ----
   if (env_ok) {
     const uint32_t* src =
         (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)env * g.map_stride));
     for (int w = lane; w < g.bits_words; w += g.L) bitsL[w] = src[w];
   }
-  for (int i = lane; i < 8; i += g.L) flag[i] = (i & 3) == 0 ? 1 : 0;  // alldone = 1, bad = 0
+  for (int i = lane; i < 12; i += g.L) flag[i] = (i & 3) == 0 ? 1 : 0;  // alldone = 1, bad = 0
   if (FR && tid < 32) ctab[tid] = code_reward(g, (uint32_t)tid);
   if (FR && tid < FR) bigrow[tid] = 0;
   __syncthreads();
@@ -631,17 +649,30 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   const int es = (int)sizeof(CellT);  // obs element size == cell size
   const long long Elong = g.E;
 
-  const int T = ROLL ? a.T : 1;
-  // actions are loaded one step ahead: step s + 1's load is issued before step s's
-  // stores, so waiting for it never waits for them (vmcnt counts both, in order)
-  const bool read_act = a.do_step && !a.use_rng;
-  int act_nx[APL];
+  // MAPFX_GEN_CARRY: bit d = neighbour d of the agent's cell blocked (an obstacle nobody
+  // stands on, or outside the grid), bit 4 + d = occupied, on the current (pre-step) map
+  uint32_t nbits[APL];
+  const auto read_nbits = [&](int k) {
+    const int cc = (r[k] + g.P) * g.pitch + c[k] + g.pl;
+    const uint32_t v0 = map[cc - g.pitch], v1 = map[cc + g.pitch], v2 = map[cc - 1], v3 = map[cc + 1];
+    const auto nb = [](uint32_t v, int d) {
+      return (v == CT::OE ? 1u << d : 0u) | ((v & CT::CNT) ? 16u << d : 0u);
+    };
+    return nb(v0, 0) | nb(v1, 1) | nb(v2, 2) | nb(v3, 3);
+  };
+  if constexpr (CARRY) {
 #pragma unroll
-  for (int k = 0; k < APL; ++k)
-    act_nx[k] = (has[k] && read_act)
-                    ? load_action(a.actions, a.act_dtype, (long long)env * N + lane + k * g.L) : 4;
+    for (int k = 0; k < APL; ++k) {
+      nbits[k] = has[k] ? read_nbits(k) : 0u;
+      if (has[k] && a.do_step && !a.use_rng && (act_nx[k] < 0 || act_nx[k] > 4))
+        atomicOr(&flag[1], 1);  // step 0's bad action (slot 0)
+    }
+    __syncthreads();  // the neighbour reads before step 0's count moves
+  }
+  int fs = 0;  // CARRY: flag slot of step s (s % 3)
   for (int s = 0; s < T; ++s) {
-    int* fl = flag + (s & 1) * 4;
+    int* fl = flag + (CARRY ? fs : (s & 1)) * 4;
+    const int fs_next = fs == 2 ? 0 : fs + 1;
     int act_in[APL];
 #pragma unroll
     for (int k = 0; k < APL; ++k) act_in[k] = act_nx[k];
@@ -671,27 +702,36 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         else
           av = act_in[k];
         if (av < 0 || av > 4) {
-          atomicOr(&fl[1], 1);
+          if (!CARRY) atomicOr(&fl[1], 1);  // (CARRY: raised during the previous step)
           av = 4;
         }
         act[k] = av;
         if (!dn[k] && av != 4) {  // __agent_step :319-342
           const int cand =
               oc[k] + (av == 0 ? -g.pitch : (av == 1 ? g.pitch : (av == 2 ? -1 : 1)));
-          const uint32_t v = map[cand];
-          if (v == CT::OE) {
+          bool blocked;
+          int pv;
+          if constexpr (CARRY) {
+            blocked = (nbits[k] >> av) & 1u;
+            pv = (int)((nbits[k] >> (4 + av)) & 1u);  // only pre > 0 is ever asked
+          } else {
+            const uint32_t v = map[cand];
+            blocked = v == CT::OE;
+            pv = (int)(v & CT::CNT);
+          }
+          if (blocked) {
             envc[k] = true;       // out of bounds or free-standing obstacle
           } else {
             nc[k] = cand;
             moved[k] = true;
-            pre[k] = (int)(v & CT::CNT);
+            pre[k] = pv;
           }
         }
         oldc[ag] = oc[k];
         newc[ag] = nc[k];
       }
     }
-    lds_barrier();  // B1: every pre-step map read is done
+    if (!CARRY) lds_barrier();  // B1: every pre-step map read is done (and the bad flag)
     STAMP(1);
     // ================= P1: move the agent counts =================
     const bool skip = (fl[1] != 0) || !a.do_step;
@@ -712,8 +752,9 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       if constexpr ((FEAT & FEAT_PRIM) != 0) rcs[ag] = (r[k] << 16) | (c[k] & 0xFFFF);
     }
     if (a.do_step && !skip && env_ok) ++tcur;
-    if (lane == 0) {  // the next step's flags: every read of them (step s - 1's) precedes B1
-      int* nf = flag + ((s + 1) & 1) * 4;
+    if (lane == 0) {  // the next step's flags: every read of them (step s - 1's, CARRY:
+      // step s - 2's) precedes B1 (CARRY: B3 of step s - 1)
+      int* nf = flag + (CARRY ? fs_next : ((s + 1) & 1)) * 4;
       nf[0] = 1;
       nf[1] = 0;
     }
@@ -817,7 +858,14 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       }
       if (a.traj_pos) ((int2*)a.traj_pos)[ai] = make_int2(r[k], c[k]);
       if (a.traj_done) a.traj_done[ai] = dn[k] ? 1 : 0;
-      if (a.avail) {  // :203-224 on the post-step map
+      if constexpr (CARRY) {
+        // the post-step neighbours: the next step's move decision, and avail (:203-224)
+        nbits[k] = read_nbits(k);
+        if (a.avail) a.avail[ai] = (uint8_t)(16u | (~nbits[k] & 15u));
+        // the next step's action (loaded at this step's start): an invalid one skips its
+        // env (:91-92), raised now so that step needs no barrier before its count moves
+        if (read_act && s + 1 < T && (act_nx[k] < 0 || act_nx[k] > 4)) atomicOr(&flag[fs_next * 4 + 1], 1);
+      } else if (a.avail) {  // :203-224 on the post-step map
         const int cc = nc[k];
         uint32_t m = 16u;
         m |= ((uint32_t)map[cc - g.pitch] != CT::OE) ? 1u : 0u;
@@ -1076,7 +1124,18 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     // B4: the autoreset's map atomics before the next step's reads; without autoreset
     // every hand-off of this step is already ordered by B3 (the tail and the fold read
     // nothing the next step writes before its B1)
-    if (ROLL && s + 1 < T && a.autoreset) lds_barrier();
+    if (ROLL && s + 1 < T && a.autoreset) {
+      lds_barrier();
+      if constexpr (CARRY) {  // the reset agents' neighbours, then B5 before the count moves
+        if (alldone && a.do_step) {
+#pragma unroll
+          for (int k = 0; k < APL; ++k)
+            if (has[k]) nbits[k] = read_nbits(k);
+        }
+        lds_barrier();
+      }
+    }
+    fs = fs_next;
   }
 
   // ---- write back the env state ----
@@ -3032,7 +3091,7 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     off += epb * g.map_env_bytes;
     off += (prim_arrays ? 4 : 2) * round_up(epb * N * 4, 16);
     off += std::max(epb * g.bits_env_bytes, round_up(epb * N * 8, 16));
-    off += round_up(epb * 8 * 4, 16);
+    off += round_up(epb * 12 * 4, 16);
     return off;
   };
   int EPB = 256 / L;
@@ -3063,7 +3122,7 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   const int rew_bytes = std::max(EPB * g.bits_env_bytes, round_up(EPB * N * 8, 16));
   off += rew_bytes;
   g.off_flag = off;
-  off += round_up(EPB * 8 * 4, 16);
+  off += round_up(EPB * 12 * 4, 16);
   g.gen_lds = off;
   // Deferred fold (rollouts with one env per block): the ring of FOLD_R code rows
   // replaces the fp64 reward row, and is kept only when the block count per CU stays.
@@ -3077,7 +3136,7 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     if (LDS_MAX / lds_f >= LDS_MAX / g.gen_lds) {
       g.fold_R = FOLD_R;
       g.off_flag = g.off_rew + ring;
-      g.off_ctab = g.off_flag + round_up(EPB * 8 * 4, 16);
+      g.off_ctab = g.off_flag + round_up(EPB * 12 * 4, 16);
       g.gen_lds = lds_f;  // step launches share the layout (the ring is unused there)
     }
   }

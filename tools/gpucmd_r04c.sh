@@ -11,3 +11,5 @@ timeout -k 10 800 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_d
 tail -1 $OUT/tests.txt
 bash tools/ab_bench.sh $OUT/ab20 3 "--gpus 1 --steps 20 --warmup 5" $L/libmapfx.so $L/libmapfx_nolag.so || exit 1
 bash tools/ab_bench.sh $OUT/ab64 2 "--gpus 1 --steps 512 --warmup 64" $L/libmapfx.so $L/libmapfx_nolag.so || exit 1
+# C5: carried neighbour bits (no B1) vs without
+bash tools/ab_bench.sh $OUT/ab_c5 2 "--config c5 --gpus 1" $L/libmapfx.so $L/libmapfx_nocarry.so || exit 1

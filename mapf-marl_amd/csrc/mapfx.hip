@@ -619,11 +619,17 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   // actions are loaded one step ahead: step s + 1's load is issued before step s's
   // stores, so waiting for it never waits for them (vmcnt counts both, in order)
   const bool read_act = a.do_step && !a.use_rng;
-  int act_nx[APL];
+  const long long Elong_ = g.E;
+  // CARRY: two steps ahead (act_nx2): step s + 1's action is checked during step s, so
+  // its load must have been issued a whole step earlier
+  int act_nx[APL], act_nx2[APL];
 #pragma unroll
-  for (int k = 0; k < APL; ++k)
+  for (int k = 0; k < APL; ++k) {
     act_nx[k] = (has[k] && read_act)
                     ? load_action(a.actions, a.act_dtype, (long long)env * N + lane + k * g.L) : 4;
+    act_nx2[k] = (CARRY && has[k] && read_act && T > 1)
+                     ? load_action(a.actions, a.act_dtype, (Elong_ + env) * N + lane + k * g.L) : 4;
+  }
   // ---- stage the bitmap, build the padded map, add the agents ----
   if (env_ok) {
     const uint32_t* src =
@@ -676,7 +682,17 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     int act_in[APL];
 #pragma unroll
     for (int k = 0; k < APL; ++k) act_in[k] = act_nx[k];
-    if (ROLL && read_act && s + 1 < T) {
+    if constexpr (CARRY) {
+#pragma unroll
+      for (int k = 0; k < APL; ++k) act_nx[k] = act_nx2[k];
+      if (read_act && s + 2 < T) {
+#pragma unroll
+        for (int k = 0; k < APL; ++k)
+          if (has[k])
+            act_nx2[k] = load_action(a.actions, a.act_dtype,
+                                     ((long long)(s + 2) * Elong + env) * N + lane + k * g.L);
+      }
+    } else if (ROLL && read_act && s + 1 < T) {
 #pragma unroll
       for (int k = 0; k < APL; ++k)
         if (has[k])
@@ -1566,9 +1582,12 @@ __device__ __forceinline__ void stage_occ_record(const uint32_t (&R)[(WIN * WIN 
 // 1 (ALT only): the step images are a 3-slot ring published one barrier late.  The step
 // wave writes step q's image in iteration q + 1 and the store waves read it after barrier
 // q + 3, so the step wave's barrier waits for everything but its own latest image writes
-// (s_waitcnt lgkmcnt(NQ)): the image stores of a step leave its critical path (round 4,
-// C2: cutting them to one store per lane measured -1.4 us per T = 20 launch).
-#define MAPFX_SPLIT_LAG (MAPFX_SPLIT_ALT && !MAPFX_SPLIT_MOVE)
+// (s_waitcnt lgkmcnt(NQ)): the image stores of a step leave its critical path.  Measured
+// round 4 (C2, same box, interleaved): T = 20 23.3 vs 23.0 us, T = 64 54.4 vs 53.5 us --
+// slower (one more barrier interval of drain, 4 KB more LDS per block), so off.  Cutting
+// the image to one store per lane (diagnostic ablation 2048) had measured -1.4 us: the
+// image's LDS traffic costs, not the step wave's wait for it.
+#define MAPFX_SPLIT_LAG 0
 #endif
 constexpr int SPLIT_NIMG = MAPFX_SPLIT_LAG ? 3 : 2;  // step images in the ring
 // step-side waves ahead of the store waves

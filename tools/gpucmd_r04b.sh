@@ -4,9 +4,17 @@
 # of the bench command each line is taken with, summarised into profiles/.
 set -o pipefail
 export TMPDIR=/tmp
+O=gpurun_out
+mkdir -p $O/r04b
+# generic rollouts with the two-deep action prefetch (MAPFX_GEN_CARRY): parity, then C5 A/B
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread \
+  -k "generic or full_size or rollout or autoreset or invalid" > $O/r04b/tests.txt 2>&1 \
+  || { grep -E "FAIL|Error" $O/r04b/tests.txt | head -30; tail -30 $O/r04b/tests.txt; exit 1; }
+tail -1 $O/r04b/tests.txt
+bash tools/ab_bench.sh $O/r04b/ab_c5 2 "--config c5 --gpus 1" mapf-marl_amd/mapfx/libmapfx.so \
+  mapf-marl_amd/mapfx/libmapfx_nocarry.so || exit 1
 bash tools/r03_profile.sh r04b_c3 --config c3 --gpus 1 --cpu-seconds 0 --per-step-steps 0 || exit 1
 bash tools/r03_profile.sh r04b_step --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --per-step-steps 200 || exit 1
-O=gpurun_out
 python3 tools/pmc_traffic.py --trace $O/r04b_c3/trace --fetch $O/r04b_c3/pmc_fetch --write $O/r04b_c3/pmc_write \
   --lds $O/r04b_c3/pmc_lds --sq $O/r04b_c3/pmc_sq --kernel "mapf_wave_kernel<5, true" --config c3 --T 64 --E 2048 \
   --tag r04_c3 --command "python3 bench.py --config c3 --gpus 1 --cpu-seconds 0 --per-step-steps 0" \
@@ -34,3 +42,5 @@ bash tools/ab_bench.sh $O/r04b_stepab 2 "--gpus 1 --steps 20 --warmup 5 --per-st
   mapf-marl_amd/mapfx/libmapfx.so mapf-marl_amd/mapfx/libmapfx_stagerec.so || true
 # MARL_PARTIAL per-phase stamps (diagnostic build)
 timeout -k 10 120 python3 tools/pstamps_partial.py > $O/r04b_pstamps.txt 2>&1 && cat $O/r04b_pstamps.txt
+# C2 split kernel, block-0 per-segment stamps (diagnostic build) at T = 64
+timeout -k 10 120 python3 tools/stamps.py > $O/r04b_c2_stamps.txt 2>&1 && cat $O/r04b_c2_stamps.txt

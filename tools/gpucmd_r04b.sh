@@ -34,12 +34,6 @@ mkdir -p $O/r04b_runner
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/r04b_runner/trace -o run --output-format csv \
   -- python3 bench.py --env runner --cpu-seconds 0 --steps 200 --warmup 100 > $O/r04b_runner/bench.json 2> $O/r04b_runner/err.txt || exit 1
 tail -c 300 $O/r04b_runner/bench.json; echo
-# MARL_PARTIAL: this round's kernel vs round 3's (carried goal distance, early lookups)
-mkdir -p $O/r04b_runner; bash tools/ab_bench.sh $O/r04b_pab 2 "--env marl_partial" mapf-marl_amd/mapfx/libmapfx.so \
-  mapf-marl_amd/mapfx/libmapfx_oldpartial.so || true
-# per-step drop-in kernel: records staged in LDS + 16-byte stores (MAPFX_DIRECT_REC=0) vs direct
-bash tools/ab_bench.sh $O/r04b_stepab 2 "--gpus 1 --steps 20 --warmup 5 --per-step-steps 200" \
-  mapf-marl_amd/mapfx/libmapfx.so mapf-marl_amd/mapfx/libmapfx_stagerec.so || true
 # MARL_PARTIAL per-phase stamps (diagnostic build)
 timeout -k 10 120 python3 tools/pstamps_partial.py > $O/r04b_pstamps.txt 2>&1 && cat $O/r04b_pstamps.txt
 # C2 split kernel, block-0 per-segment stamps (diagnostic build) at T = 64

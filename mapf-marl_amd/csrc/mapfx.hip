@@ -262,8 +262,10 @@ __device__ __forceinline__ __attribute__((unused)) uint32_t lds_addr(const void*
 #ifndef MAPFX_GEN_CARRY
 // 1: generic rollouts carry each agent's 4 neighbour cells (blocked / occupied bits) from
 // the post-step map of one step to the move decision of the next, and raise an invalid
-// next action's flag one step early, so a step needs no pre-step map read and no B1
-#define MAPFX_GEN_CARRY 1
+// next action's flag one step early (actions prefetched two steps ahead), so a step needs
+// no pre-step map read and no B1.  Measured round 4 at C5 (interleaved, same box): 0.437
+// vs 0.423 ms per T = 64 launch -- slower, so off.
+#define MAPFX_GEN_CARRY 0
 #endif
 #ifndef MAPFX_OCC_GROUPS
 #define MAPFX_OCC_GROUPS 1  // u16 occupancy windows as 8-row groups of 16-byte stores
@@ -1266,7 +1268,7 @@ __device__ __forceinline__ void fast_row_prefetch(const Geo& g, const uint32_t* 
 }
 template <int MAXW, int RPF>
 __device__ inline void build_map_rows_fast(const Geo& g, uint32_t* map32, const uint32_t* src, int lane,
-                                           int nl, const uint32_t (&pf)[RPF][3]) {
+                                           int nl, const uint32_t (&pf)[RPF][3], uint32_t* map32b = nullptr) {
   const int wpr = g.wpr, pl = g.pl, e = g.pl + g.W, last = g.bits_words - 1;
   const uint64_t wmask = g.W < 64 ? (1ull << g.W) - 1ull : ~0ull;
   // one padded row from its bitmap words w0..w2 (the words covering bits rr*W ..)
@@ -1282,13 +1284,16 @@ __device__ inline void build_map_rows_fast(const Geo& g, uint32_t* map32, const 
       hi = (uint32_t)(rb >> (64 - pl)) | (e <= 64 ? ~0u : (e < 96 ? ~0u << (e - 64) : 0u));
     }
     uint2* row2 = (uint2*)(map32 + pr * wpr);
+    uint2* row2b = map32b ? (uint2*)(map32b + pr * wpr) : nullptr;  // (a second copy: MAPFX_SPLIT_DBM)
 #pragma unroll
     for (int j = 0; j < MAXW / 2; ++j) {
       if (2 * j < wpr) {
         const int w = 2 * j;  // cells 4w .. 4w+7 of the padded row
         const uint32_t n0 = w < 16 ? (uint32_t)(lo >> (4 * w)) : hi >> (4 * w - 64);
         const uint32_t n1 = w + 1 < 16 ? (uint32_t)(lo >> (4 * w + 4)) : hi >> (4 * w - 60);
-        row2[j] = make_uint2(cells_of_nibble(n0 & 0xFu), cells_of_nibble(n1 & 0xFu));
+        const uint2 cw = make_uint2(cells_of_nibble(n0 & 0xFu), cells_of_nibble(n1 & 0xFu));
+        row2[j] = cw;
+        if (row2b) row2b[j] = cw;
       }
     }
   };
@@ -1590,6 +1595,19 @@ __device__ __forceinline__ void stage_occ_record(const uint32_t (&R)[(WIN * WIN 
 #define MAPFX_SPLIT_LAG 0
 #endif
 constexpr int SPLIT_NIMG = MAPFX_SPLIT_LAG ? 3 : 2;  // step images in the ring
+#ifndef MAPFX_SPLIT_DBM
+// 1 (ALT, no LAG / MOVE): two agent-count maps, M0 for even steps and M1 for odd ones.
+// Step s moves the counts of map s & 1 from the positions after step s - 2 to those after
+// step s, so a step's map stays intact for the whole next barrier interval: the store
+// waves read a step's window rows from it themselves, and the step wave hands over only
+// a 16-byte info word per agent (and its edge count one step later) instead of the info
+// word plus the raw window rows (round 4: the step wave's image stores cost ~1.4 us of a
+// C2 T = 20 launch).  The step wave reads the 4 neighbour bytes of its
+// agent's new cell, not its 5 window rows.
+#define MAPFX_SPLIT_DBM (MAPFX_SPLIT_ALT && !MAPFX_SPLIT_LAG && !MAPFX_SPLIT_MOVE)
+#endif
+constexpr int SPLIT_DBM_INFO = 2 * 64 * 16;  // DBM: info words of two steps
+constexpr int SPLIT_DBM_EDGE = 2 * 64;       // DBM: edge counts of two steps
 // step-side waves ahead of the store waves
 #define MAPFX_SPLIT_SW0 (MAPFX_SPLIT_MOVE ? 2 : 1)
 constexpr int SPLIT_RING_LDS = 2 * 64 * 16;  // MOVE -> MAP ring: 2 steps x 64 lanes x u32x4
@@ -1865,6 +1883,136 @@ __device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a
   }
 }
 
+// The store waves under MAPFX_SPLIT_DBM.  Wave `par` takes the steps q with q % 2 == par:
+//   a(q), the interval after barrier q + 1: step q's info word (written by the step wave
+//     in its iteration q) and the agent's window rows read from map q & 1 -- intact until
+//     the step wave's iteration q + 2 moves that map's counts again -- to the record, staged
+//     in the wave's LDS image, and the node flag;
+//   b(q), the interval after barrier q + 2: the edge count (the step wave computes it in
+//     iteration q + 1), the reward code, the staged record out with lane-contiguous
+//     16-byte stores, every per-agent and per-env output, and every 16th step the fold.
+template <int WIN, int LL, bool OCC>
+__device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a, const unsigned char* m0,
+                                                     const unsigned char* m1, const unsigned char* info,
+                                                     const unsigned char* ering, unsigned char* own,
+                                                     double* rtab, unsigned char* codes, int env0,
+                                                     int lane, int par) {
+  typedef __attribute__((address_space(1))) unsigned char gbyte;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef int i32x2 __attribute__((ext_vector_type(2)));
+  constexpr int H2 = WIN / 2, REC = OCC ? WIN * WIN : 2 * WIN * WIN;
+  constexpr int RCH = 4 * REC;  // 16-byte chunks of the wave's 64 records
+  constexpr int NRC = (RCH + 63) / 64;
+  const int T = a.T;
+  const uint32_t E = (uint32_t)g.E, EN = E * (uint32_t)LL;
+  const int slot = lane / LL, ag = lane % LL;
+  const uint32_t env = (uint32_t)(env0 + slot), ag0 = (uint32_t)env0 * LL;
+  const u32x4* ost = (const u32x4*)__builtin_assume_aligned(own, 16);
+  const u32x4* inf = (const u32x4*)__builtin_assume_aligned(info, 16);
+  const int pitch = g.pitch, wpr = g.pitch >> 2;
+  uint32_t k_nc = 0, k_nb = 0, k_fl = 0, k_t = 0, k_node = 0;  // step q's, kept from a to b
+
+  for (int c = lane + 64 * par; c < 256; c += 128) {  // the code reward table (as the ALT waves)
+    double rr = 0.0;  // exact fp64 op order of the reference
+    if (c & SF_LIVE) {
+      if (!(c & SF_DNOLD)) {
+        if (c & SF_ENVC) rr = rr + g.collide_rew;
+        rr = rr + g.step_rew;
+      }
+      rr = rr + g.collide_rew * (double)(c & 1);
+      rr = rr + g.collide_rew * (double)(c >> 4);
+    }
+    rtab[c] = rr;
+  }
+  auto fold_batch = [&](uint32_t q0, int cnt) {  // one (env, step) per lane, agent order
+    const int j = lane & 15, e = lane >> 4;
+    if (j < cnt) {
+      const u32x4 cv = *(const u32x4*)__builtin_assume_aligned(codes + ((q0 + j) & 31) * 64 + e * 16, 16);
+      const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w};
+      double v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = rtab[(cw[i >> 2] >> (8 * (i & 3))) & 0xFFu];
+      double R = 0.0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) R = R + v[i];
+      const uint32_t ei = (q0 + j) * E + (uint32_t)env0 + e;
+      split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), R);
+      if (a.reward_f32) a.reward_f32[ei] = (float)R;
+    }
+  };
+  auto part_a = [&](uint32_t q) {
+    const u32x4 iv = inf[(q & 1) * 64 + lane];
+    const uint32_t* m32 = (const uint32_t*)((q & 1) ? m1 : m0) + (slot * g.map_env_bytes >> 2);
+    const int nc = (int)iv.x;
+    const int w0 = (nc - H2 * pitch - H2) >> 2;
+    uint32_t qx[3 * WIN];
+#pragma unroll
+    for (int y = 0; y < WIN; ++y) {
+      qx[y] = m32[w0 + y * wpr];
+      qx[WIN + y] = m32[w0 + y * wpr + 1];
+      qx[2 * WIN + y] = WIN > 5 ? m32[w0 + y * wpr + 2] : 0u;
+    }
+    const int o = (nc - H2) & 3;
+    if constexpr (OCC) {
+      uint32_t R[(WIN * WIN + 3) / 4 + 1];
+      occ_words<WIN>(qx, o, R);
+      stage_occ_record<WIN>(R, lds_addr(own + lane * REC));
+    } else {
+      uint32_t R[4 * WIN];
+      window_regs<WIN>(qx, o, R);
+      stage_record<WIN>(R, own + lane * REC);
+    }
+    // node collision (:344-362): post-step count = c - 1 + obstacle >= 2 (centre cell)
+    const uint32_t ctr = (__builtin_amdgcn_alignbyte(qx[WIN + H2], qx[H2], o) >> (8 * H2)) & 0xFFu;
+    k_node = ((ctr & 0x7Fu) + (ctr >> 7) >= 3u && !(iv.z & SF_SKIP)) ? 1u : 0u;
+    k_nc = iv.x, k_nb = iv.y, k_fl = iv.z, k_t = iv.w;
+  };
+  auto part_b = [&](uint32_t q) {
+    u32x4 rv[NRC];
+#pragma unroll
+    for (int k = 0; k < NRC; ++k) rv[k] = ost[(k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0];
+    const uint32_t edge = ering[(q & 1) * 64 + lane];
+    codes[(q & 31) * 64 + lane] =
+        (unsigned char)(k_node | (k_fl & (SF_LIVE | SF_DNOLD | SF_ENVC)) | ((edge & 0xFu) << 4));
+    gbyte* rec = (gbyte*)(OCC ? a.obs_window_occ : a.obs_window) + (q * EN + ag0) * (uint32_t)REC;
+#pragma unroll
+    for (int k = 0; k < NRC; ++k)
+      if (k < NRC - 1 || lane + 64 * k < RCH)
+        split_store((__attribute__((address_space(1))) u32x4*)(rec + 16u * (lane + 64 * k)), rv[k]);
+    const uint32_t fl = k_fl;
+    const uint32_t nzn = (((k_nb & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
+    const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
+    const uint32_t ai = q * EN + ag0 + lane;
+    const int2 rc = padded_cell_rc(g, (int)k_nc);
+    split_store((__attribute__((address_space(1))) i32x2*)((gbyte*)a.traj_pos + 8u * ai), i32x2{rc.x, rc.y});
+    split_store((gbyte*)a.node + ai, (unsigned char)k_node);
+    split_store((gbyte*)a.edge + ai, (unsigned char)edge);
+    split_store((gbyte*)a.avail + ai, (unsigned char)availm);
+    split_store((gbyte*)a.traj_done + ai, (unsigned char)(fl & SF_DONE));
+    if (ag == LL - 1) {
+      const uint32_t ei = q * E + env;
+      split_store((__attribute__((address_space(1))) int*)((gbyte*)a.traj_t + 4u * ei), (int)k_t);
+      split_store((gbyte*)a.term + ei, (unsigned char)((fl & SF_ALLDONE) ? 1 : 0));
+      if (a.err && (fl & SF_SKIP)) atomicCAS(a.err, 0, (int)env + 1);
+    }
+    // the batch ends here: every code of it is in the ring (this wave's b(q) just now,
+    // the other wave's b(q - 1) before the last barrier)
+    if ((q & 15u) == 15u || q + 1 == (uint32_t)T) {
+      wave_fence();
+      fold_batch(q & ~15u, (int)(q & 15u) + 1);
+    }
+  };
+
+  const int rounds = T > 0 ? T + 1 : 0;
+  for (int s = 1; s <= rounds; ++s) {
+    split_barrier();
+    if (MAPFX_ABLATE & 256) continue;
+    const int q = s - 1;  // a(q) now; b(q - 1) by the other parity
+    if (q < T && (q & 1) == par) part_a((uint32_t)q);
+    else if (q >= 1 && ((q - 1) & 1) == par) part_b((uint32_t)(q - 1));
+  }
+}
+
 template <int WIN, int LL, int ROLE, bool OCC = false>
 __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, unsigned char* sp,
                                                  unsigned char* own, int env0, int lane) {
@@ -2031,7 +2179,9 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
         const int bl = l64 % LL + LL * (threadIdx.x >> 6);
         fast_row_prefetch<1>(g, src, bl, LL * MAPFX_SPLIT_WAVES, pf);
         build_map_rows_fast<MAPFX_FAST_WPR, 1>(g, (uint32_t*)(lds + g.wv_off_map + sl * g.map_env_bytes), src,
-                                               bl, LL * MAPFX_SPLIT_WAVES, pf);
+                                               bl, LL * MAPFX_SPLIT_WAVES, pf,
+                                               MAPFX_SPLIT_DBM ? (uint32_t*)(lds + g.wv_off_split + sl * g.map_env_bytes)
+                                                               : nullptr);
       }
       split_barrier();
       unsigned char* sp = lds + g.wv_off_split;
@@ -2039,7 +2189,15 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
       constexpr int RECB = OCC ? WIN * WIN : 2 * WIN * WIN;  // one wave's staged image: 64 * RECB
       double* rtab = (double*)(own + 2 * 64 * RECB);          // ALT: reward table + code ring
       const int par = (int)(threadIdx.x >> 6) - MAPFX_SPLIT_SW0;  // ALT: this wave's step parity
-      if (MAPFX_SPLIT_ALT)
+      if (MAPFX_SPLIT_DBM) {  // [M1: 64 / LL maps][info: 2 steps][edge: 2 steps][staged records][fold]
+        unsigned char* m1 = lds + g.wv_off_split;
+        unsigned char* inf = m1 + (64 / LL) * g.map_env_bytes;
+        unsigned char* eri = inf + SPLIT_DBM_INFO;
+        unsigned char* ownd = eri + SPLIT_DBM_EDGE;
+        double* rt = (double*)(ownd + 2 * 64 * RECB);
+        split_store_wave_dbm<WIN, LL, OCC>(g, a, lds + g.wv_off_map, m1, inf, eri, ownd + par * 64 * RECB, rt,
+                                           (unsigned char*)(rt + 256), e0, threadIdx.x & 63, par);
+      } else if (MAPFX_SPLIT_ALT)
         split_store_wave_alt<WIN, LL, OCC>(g, a, sp, own + par * 64 * RECB, rtab,
                                            (unsigned char*)(rtab + 256), e0, threadIdx.x & 63, par);
       else if (MAPFX_SPLIT_WAVES == 2) split_store_wave<WIN, LL, ROLE_ALL, OCC>(g, a, sp, own, e0, threadIdx.x & 63);
@@ -2151,8 +2309,15 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
   }
   if (!g.wv_fast) wave_fence();
   PSTAMP(1);
-  if (g.wv_fast) build_map_rows_fast<MAPFX_FAST_WPR, RPF>(g, map32, bsrc, bl, bnl, pfw);
+  // MAPFX_SPLIT_DBM: the odd steps' map M1 of this env (at the start of the split region)
+  constexpr bool DBM = SPLIT && MAPFX_SPLIT_DBM && WIN > 0;
+  uint32_t* m1_32 = DBM ? (uint32_t*)(lds + g.wv_off_split + slot * g.map_env_bytes) : nullptr;
+  if (g.wv_fast) build_map_rows_fast<MAPFX_FAST_WPR, RPF>(g, map32, bsrc, bl, bnl, pfw, m1_32);
   else build_map_rows_c(g, map32, bitsL, ag, L);
+  if (DBM && !g.wv_fast) {  // (the fallback builder fills M0 alone: copy it)
+    wave_fence();
+    for (int w = ag; w < (g.map_env_bytes >> 2); w += L) m1_32[w] = map32[w];
+  }
   if constexpr (SPLIT) split_barrier();  // + the store waves' rows
   else wave_fence();
   PSTAMP(2);
@@ -2168,6 +2333,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
     fast = __ballot(((map[cur] | map[icell]) & 0x80u) != 0) == 0;
   }
   if (has && !is_map) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
+  if (DBM && has) atomicAdd(&m1_32[cur >> 2], 1u << ((cur & 3) * 8));
   wave_fence();
 
   const auto cell_rc = [&](int cell) {  // padded cell -> (row, col); cell < 2^16, pitch < 256
@@ -2532,6 +2698,102 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
     }
   }
 
+  if constexpr (DBM) {
+    // ---- MAPFX_SPLIT_DBM step wave: map s & 1 is moved from the positions after step
+    // s - 2 to those after step s; the store waves read step s's window rows from it ----
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    unsigned char* m1 = (unsigned char*)m1_32;
+    u32x4* info = (u32x4*)__builtin_assume_aligned(lds + g.wv_off_split + EPW * g.map_env_bytes, 16);
+    unsigned char* ering = (unsigned char*)(info + 128);
+    int cp0 = cur, cp1 = cur;  // where this lane's agent is counted in M0 / M1
+    bool reset_pending = false;
+    for (int s = 0; s < T; ++s) {
+      const bool odd = (s & 1) != 0;
+      unsigned char* mp = odd ? m1 : map;
+      uint32_t* mp32 = (uint32_t*)mp;
+      if (a.autoreset && __ballot(reset_pending)) {
+        // the last step ended these envs' episodes (their agents are back at init_pos,
+        // mapf_gridworld.py:70-83): count them there in this step's map -- intact since
+        // barrier s - 1's readers are done -- and read their neighbours
+        if (reset_pending) {
+          const int cpi = odd ? cp1 : cp0;
+          atomicAdd(&mp32[cpi >> 2], cpi != cur ? 0u - (1u << ((cpi & 3) * 8)) : 0u);
+          atomicAdd(&mp32[cur >> 2], cpi != cur ? 1u << ((cur & 3) * 8) : 0u);
+          if (odd) cp1 = cur; else cp0 = cur;
+        }
+        wave_fence();
+        if (reset_pending)
+          nb = (uint32_t)mp[cur - pitch] | ((uint32_t)mp[cur + pitch] << 8) |
+               ((uint32_t)mp[cur - 1] << 16) | ((uint32_t)mp[cur + 1] << 24);
+        reset_pending = false;
+      }
+      const int act = next_action(s);
+      // A: move decision on the pre-step neighbours (:319-342), this map's count moves
+      const int oc = cur;
+      const bool mv = !dn && (uint32_t)act < 4u;
+      const uint32_t v = mv ? ((nb >> ((act & 3) * 8)) & 0xFFu) : 0u;
+      const bool envc = mv && (v & 0x7Fu) == 0u;
+      const bool skip = (__ballot(act == 0xFF) & envmask) != 0;
+      const bool moved = mv && (v & 0x7Fu) != 0u && !skip;
+      int dlt = (act & 2) ? 1 : pitch;
+      dlt = (act & 1) ? dlt : -dlt;
+      const int nc = moved ? oc + dlt : oc;
+      dep[oc] = (unsigned char)(moved ? (uint32_t)act : 0x7Fu);
+      const int cpi = odd ? cp1 : cp0;
+      atomicAdd(&mp32[cpi >> 2], cpi != nc ? 0u - (1u << ((cpi & 3) * 8)) : 0u);
+      atomicAdd(&mp32[nc >> 2], cpi != nc ? 1u << ((nc & 3) * 8) : 0u);
+      if (odd) cp1 = nc; else cp0 = nc;
+      cur = nc;
+      // B: the new cell's 4 neighbours (the next move decision, avail) and the pre-step
+      // occupant's move (the edge test)
+      const uint32_t n_up = mp[nc - pitch], n_dw = mp[nc + pitch], n_lf = mp[nc - 1], n_rt = mp[nc + 1];
+      const uint32_t dj = dep[nc];
+      // C: step s - 1's edge count (:364-383), for the store wave's b part
+      if (s > 0) {
+        const int e = edge_of();
+        ering[((s - 1) & 1) * 64 + lane64] = (unsigned char)(e > 255 ? 255 : e);
+      }
+      // D: dones, t (:112-117), the step's info word
+      const uint32_t nbn = n_up | (n_dw << 8) | (n_lf << 16) | (n_rt << 24);
+      const bool dn_old = dn;
+      const bool live = !skip;
+      if (live && nc == gcell) dn = true;
+      if (live && tcur + 1 >= g.limit) dn = true;
+      if (live && !dn_old) ++st;
+      if (!skip) ++tcur;
+      const bool alldone = (__ballot(!dn) & envmask) == 0;
+      const uint32_t fl = (dn ? SF_DONE : 0u) | (live ? SF_LIVE : 0u) | (dn_old ? SF_DNOLD : 0u) |
+                          (envc ? SF_ENVC : 0u) | (skip ? SF_SKIP : 0u) | (alldone ? SF_ALLDONE : 0u);
+      info[(s & 1) * 64 + lane64] = u32x4{(uint32_t)nc, nbn, fl, (uint32_t)tcur};
+      q_oc = oc;
+      q_nc = nc;
+      q_act = act;
+      q_pre = (int)(v & 0x7Fu) - 1 + (int)(v >> 7);
+      q_dj = dj;
+      q_moved = moved;
+      nb = nbn;
+      if (a.autoreset && alldone) {  // counted at init_pos in the next step's map
+        const int2 p = ((const int2*)a.init_pos)[oa];
+        cur = cell0 + p.x * pitch + p.y;
+        dn = false;
+        st = 0;
+        tcur = 0;
+        reset_pending = true;
+      }
+      split_barrier();  // info s, map s & 1, edge s - 1 -> store waves
+    }
+    if (T > 0) {  // the last step's edge count
+      const int e = edge_of();
+      ering[((T - 1) & 1) * 64 + lane64] = (unsigned char)(e > 255 ? 255 : e);
+    }
+    split_barrier();
+    ((int2*)a.pos)[oa] = cell_rc(cur);
+    a.done[oa] = dn ? 1 : 0;
+    if (a.steps) a.steps[oa] = st;
+    if (ag == 0) a.t[env] = tcur;
+    return;
+  }
+
   for (int s = 0; s < T; ++s) {
     const int act = next_action(s);
     STAMP(0);
@@ -2894,8 +3156,13 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
                            (uintptr_t)a.traj_done | (uintptr_t)a.reward | (uintptr_t)a.traj_t;
     // + staged-record images of the store wave (2 x 64 records)
     // (+ ALT: the 256-entry reward table and the 32-step code ring)
-    const int split_lds = g.wv_lds + SPLIT_NIMG * g.wv_split_buf + 2 * 64 * (occ ? g.wlen / 2 : g.wlen) +
-                          (MAPFX_SPLIT_ALT ? SPLIT_FOLD_LDS : 0) + (MAPFX_SPLIT_MOVE ? SPLIT_RING_LDS : 0);
+    const int split_lds =
+        MAPFX_SPLIT_DBM
+            // M1 (the odd steps' maps of the wave's envs), info + edge rings, staged records, fold
+            ? g.wv_lds + g.EPW * g.map_env_bytes + SPLIT_DBM_INFO + SPLIT_DBM_EDGE +
+                  2 * 64 * (occ ? g.wlen / 2 : g.wlen) + SPLIT_FOLD_LDS
+            : g.wv_lds + SPLIT_NIMG * g.wv_split_buf + 2 * 64 * (occ ? g.wlen / 2 : g.wlen) +
+                  (MAPFX_SPLIT_ALT ? SPLIT_FOLD_LDS : 0) + (MAPFX_SPLIT_MOVE ? SPLIT_RING_LDS : 0);
     const bool split = MAPFX_SPLIT && runner && fullw && g.L == 16 && g.wv_split_buf > 0 &&
                        split_lds <= 64 * 1024 && (al16 & 15) == 0;
     KernelFn fn = pick_wave_kernel((a.obs_window || occ) ? g.window : 0, roll, fullw, runner, g.L, split, occ);

@@ -800,58 +800,51 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
 
   PST(0);
   const long long oa = (long long)env * N + ag;
-  // ---- state ----
-  int r = 0, c = 0, gr = 0, gc = 0, ir = 0, ic = 0, steps = 0, gcost = -1, edge = 0;
+  // ---- every global read of the launch issued up front, branch-free (idle lanes read
+  // entry 0 and ignore it), the bitmap's first words first: LDS staging then waits for
+  // them alone, the goal-distance lookups for the position and action alone, and the
+  // rest lands during the map build ----
+  const long long oc_ = has ? oa : 0;
+  const int ec_ = env_ok ? env : 0;
+  const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)ec_ * g.map_stride));
+  const uint32_t bw0 = bsrc[ag < g.bits_words ? ag : 0];  // this lane's first bitmap word
+  const int2 q = ((const int2*)a.goal)[oc_];
+  const int2 ip = ((const int2*)a.init_pos)[oc_];
+  const int2 p0 = ((const int2*)a.pos)[oc_];
+  int act = (a.do_step && has) ? step_action(a, env, ag, oa) : 4;  // the step's action
+  const int pd0 = a.pdist ? a.pdist[oc_] : PD_NONE;
+  const int steps0 = a.steps[oc_];
+  const uint8_t at_goal0 = a.at_goal[oc_], dn0 = a.done[oc_], node0 = a.node[oc_];
+  const int gcost0 = a.goal_cost[oc_], edge0 = a.edge[oc_];
+  const int t0 = a.t[ec_], total0 = a.total_coll[ec_];
+  const uint8_t term0 = a.terminated[ec_];
+  const bool reset_me = env_ok && a.do_reset && (!a.reset_mask || a.reset_mask[ec_]);
+  // ---- state (:125-163 for a reset env) ----
+  const int gr = q.x, gc = q.y, ir = ip.x, ic = ip.y;
+  int r = 0, c = 0, steps = 0, gcost = -1, edge = 0;
   int pd = PD_NONE;  // goal distance of the current cell (carried)
   bool at_goal = false, dn = false;
   uint32_t node = 0;
-  int tcur = 0, total = 0;
-  bool term = false;
-  bool reset_me = false;
-  if (env_ok) {
-    reset_me = a.do_reset && (!a.reset_mask || a.reset_mask[env]);
-    tcur = a.t[env];
-    term = a.terminated[env] != 0;
-    total = a.total_coll[env];
-  }
   if (has) {
-    const int2 q = ((const int2*)a.goal)[oa];
-    const int2 ip = ((const int2*)a.init_pos)[oa];
-    gr = q.x;
-    gc = q.y;
-    ir = ip.x;
-    ic = ip.y;
-    if (reset_me) {  // :125-163
-      r = ir;
-      c = ic;
-    } else {
-      const int2 p = ((const int2*)a.pos)[oa];
-      r = p.x;
-      c = p.y;
-      steps = a.steps[oa];
-      at_goal = a.at_goal[oa] != 0;
-      dn = a.done[oa] != 0;
-      gcost = a.goal_cost[oa];
-      node = a.node[oa];
-      edge = a.edge[oa];
-      if (a.pdist) pd = a.pdist[oa];
+    r = reset_me ? ir : p0.x;
+    c = reset_me ? ic : p0.y;
+    if (!reset_me) {
+      steps = steps0;
+      at_goal = at_goal0 != 0;
+      dn = dn0 != 0;
+      gcost = gcost0;
+      node = node0;
+      edge = edge0;
+      pd = pd0;
     }
   }
-  // the step's action, loaded with the state (its lookup below needs it)
-  int act = 4;
-  if (a.do_step && has) {
-    act = step_action(a, env, ag, oa);
-    if (act < 0 || act > 4) act = -1;
-  }
-  if (reset_me) {
-    tcur = 0;
-    term = false;
-    total = 0;
-  }
+  if (act < 0 || act > 4) act = -1;
+  int tcur = (env_ok && !reset_me) ? t0 : 0, total = (env_ok && !reset_me) ? total0 : 0;
+  bool term = env_ok && !reset_me && term0 != 0;
   // ---- LDS map (c format) + dep map (obstacle flag in bit 7) ----
   if (env_ok) {
-    const uint32_t* src = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)env * g.map_stride));
-    for (int w = ag; w < g.bits_words; w += g.L) bitsL[w] = src[w];
+    if (ag < g.bits_words) bitsL[ag] = bw0;
+    for (int w = ag + g.L; w < g.bits_words; w += g.L) bitsL[w] = bsrc[w];  // maps past 16 x 32 words
   }
   // goal-path distances (:227-233): the move target's entry, speculatively (used when the
   // agent moves), and the current cell's when no carried value applies -- issued here, so

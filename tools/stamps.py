@@ -46,6 +46,11 @@ def main():
     print("  %-18s %7.0f %7.0f" % ("loop+actions", np.median(nxt), nxt.mean()))
     tot = st[2:, 0] - st[1:-1, 0]
     print("  %-18s %7.0f %7.0f" % ("step total", np.median(tot), tot.mean()))
+    # the first steps of a launch against the rest (cold instruction / scalar caches,
+    # every block in the same phase)
+    per = st[1:, 0] - st[:-1, 0]
+    print("  step totals, steps 0..9:", " ".join("%d" % v for v in per[:10]),
+          "| median of steps 10..%d: %.0f" % (T - 2, np.median(per[10:])))
     if st[2:T - 1, 5].any():  # store-wave split: busy time of each wave per barrier interval
         rel = st[1:T - 2, 6]          # release of barrier s (the step wave's stamp 6 of s - 1)
         rows = slice(2, T - 1)

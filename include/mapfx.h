@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MAPFX_ABI_VERSION 3
+#define MAPFX_ABI_VERSION 4
 
 /* error codes */
 #define MAPFX_OK 0
@@ -186,7 +186,7 @@ int mapfx_gen_actions(mapfx_t* h, uint64_t seed, int32_t t0, int32_t T, int8_t* 
  * done_bits[T][E][ceil(N/8)] with bit (a & 7) of byte a >> 3 = traj_done[..][a].
  * Together with the env's reward this is the state the obs follow from: rank 0
  * rebuilds any step's window / full / PRIMAL observation with mapfx_observe on the
- * unpacked positions.  ABI 3 addition. */
+ * unpacked positions.  ABI 4 addition. */
 int mapfx_pack_compact(mapfx_t* h, int32_t T, const int32_t* traj_pos, const uint8_t* traj_done,
                        uint16_t* cell, uint8_t* done_bits, void* stream);
 

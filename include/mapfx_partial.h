@@ -81,7 +81,15 @@ typedef struct mapfx_partial_state {
                                _old_pdist, :227-233): a step reads it as opd and looks
                                up only a moving agent's npd; reset / observe refresh
                                it from the table.  INT32_MIN (never reset) or a NULL
-                               pointer: looked up.  Appended in ABI 3.            */
+                               pointer: looked up.  Appended in ABI 4.            */
+  int16_t* pnbr;            /* [E][N][4] goal_dist of the 4 neighbours (up, down,
+                               left, right; an off-grid entry is unused) of each
+                               agent's current cell, written with pdist by every
+                               launch: a step
+                               takes a moving agent's npd from it instead of a
+                               dependent table lookup.  Used only with pdist and
+                               int16 tables (H*W <= 32767); NULL: looked up.
+                               Appended in ABI 4.                                  */
 } mapfx_partial_state;
 
 /* Per-call outputs (device, caller-owned; NULL = not produced). */

@@ -67,7 +67,7 @@ typedef struct mapfx_runner_state {
   int32_t* bs_inv;       /* [B] row of env b in bs, -1 when b is not in it: the fused
                             step (mapfx_runner_step) reads env b's actions from row
                             bs_inv[b] of the MAC's output and writes its actions rows
-                            there, so no separate actions pass runs (appended in ABI 3) */
+                            there, so no separate actions pass runs (appended in ABI 4) */
 } mapfx_runner_state;
 
 /* reset(): every env's observations (from `out` of mapfx_partial_reset) into row

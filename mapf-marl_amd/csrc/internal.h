@@ -26,7 +26,29 @@ typedef struct mapfx_runner_acts {
   float* ep_onehot;
   long long ep_onehot_sb, ep_onehot_st;
   int ts;
+  // runner_post_kernel's work for the envs running before the step (alive[e] != 0),
+  // fused into the env step's write-back (alive NULL: not fused): the reward /
+  // terminated rows at ts, returns, lengths, alive / alive_prev, and the state /
+  // avail_actions / filled rows at ts + 1 (ep_state / ep_avail / ep_filled point at
+  // that time row; NULL when ts + 1 == max_t or the field is absent)
+  uint8_t* alive;
+  uint8_t* alive_prev;
+  double* ep_return;
+  int64_t* ep_length;
+  float* ep_reward;
+  long long ep_reward_sb, ep_reward_st;
+  uint8_t* ep_term;
+  long long ep_term_sb, ep_term_st;
+  float* ep_state;
+  long long ep_state_sb;
+  int32_t* ep_avail;
+  long long ep_avail_sb;
+  int64_t* ep_filled;
+  long long ep_filled_sb;
 } mapfx_runner_acts;
+// 1 when mapfx_partial_step_runner can take the post pass (mapfx_runner_acts.alive):
+// the one-wave-per-env-group kernel; the workgroup path (N > 64, a side > 256) cannot
+int mapfx_partial_fuses_post(const mapfx_partial_t* h);
 int mapfx_partial_step_runner(mapfx_partial_t* h, const mapfx_partial_state* st, const void* actions,
                               int action_dtype, const mapfx_runner_acts* ra, const mapfx_partial_out* out,
                               float* obs_rows, long long obs_env_stride, const uint8_t* obs_mask,

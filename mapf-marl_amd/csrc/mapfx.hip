@@ -2005,6 +2005,13 @@ __device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a
 
   const int rounds = T > 0 ? T + 1 : 0;
   for (int s = 1; s <= rounds; ++s) {
+#ifdef MAPFX_STAMPS  // diagnostic: end of round s - 1's work (columns 5 / 7 of row s - 1)
+    if (s > 1) {
+      unsigned long long t_;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+      if (blockIdx.x == 0 && lane == 0 && s - 1 < 256) g_stamps[(s - 1) * 8 + 5 + 2 * par] = t_;
+    }
+#endif
     split_barrier();
     if (MAPFX_ABLATE & 256) continue;
     const int q = s - 1;  // a(q) now; b(q - 1) by the other parity
@@ -2728,6 +2735,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
         reset_pending = false;
       }
       const int act = next_action(s);
+      STAMP(0);
       // A: move decision on the pre-step neighbours (:319-342), this map's count moves
       const int oc = cur;
       const bool mv = !dn && (uint32_t)act < 4u;
@@ -2744,15 +2752,18 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
       atomicAdd(&mp32[nc >> 2], cpi != nc ? 1u << ((nc & 3) * 8) : 0u);
       if (odd) cp1 = nc; else cp0 = nc;
       cur = nc;
+      STAMP(2);
       // B: the new cell's 4 neighbours (the next move decision, avail) and the pre-step
       // occupant's move (the edge test)
       const uint32_t n_up = mp[nc - pitch], n_dw = mp[nc + pitch], n_lf = mp[nc - 1], n_rt = mp[nc + 1];
       const uint32_t dj = dep[nc];
+      STAMP(1);
       // C: step s - 1's edge count (:364-383), for the store wave's b part
       if (s > 0) {
         const int e = edge_of();
         ering[((s - 1) & 1) * 64 + lane64] = (unsigned char)(e > 255 ? 255 : e);
       }
+      STAMP(3);
       // D: dones, t (:112-117), the step's info word
       const uint32_t nbn = n_up | (n_dw << 8) | (n_lf << 16) | (n_rt << 24);
       const bool dn_old = dn;
@@ -2780,7 +2791,9 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
         tcur = 0;
         reset_pending = true;
       }
+      STAMP(4);
       split_barrier();  // info s, map s & 1, edge s - 1 -> store waves
+      STAMP(6);
     }
     if (T > 0) {  // the last step's edge count
       const int e = edge_of();

@@ -18,8 +18,10 @@
 // LDS for the launch; state round-trips HBM between calls.  N > 64 or a side > 256
 // (the reference's larger maps and agent counts) take partial_wg_kernel: one
 // workgroup per env, the agents' cells in an LDS hash table, the map in HBM.  Every fp64 value is
-// computed in the reference's operation order; sqrt(int) and the completion bonus
-// come from host-libm LUTs (math.sqrt / float ** int are correctly rounded there).
+// computed in the reference's operation order; the completion bonus comes from a host-libm
+// LUT (float ** int), sqrt(int) from the device's correctly rounded fp64 sqrt once
+// mapfx_partial_create has checked it against host libm on every argument the launch can
+// use (else from a host-libm LUT too).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -41,23 +43,59 @@
 
 #ifdef PARTIAL_STAMPS
 // Diagnostic build only (never the shipped library): s_memtime stamps of partial_kernel's
-// phases, block 0 / lane 0, read back with mapfx_partial_debug_stamps().
+// phases, block 0 / lane 0, read back with mapfx_partial_debug_stamps().  The stamps stay
+// in registers until the end (PST_FLUSH): a store per stamp would make the kernel's
+// waits on the vector-memory counter wait for it too.
 __device__ unsigned long long g_pstamps[16];
-#define PST(k)                                                                   \
-  do {                                                                           \
-    __builtin_amdgcn_sched_barrier(0);                                           \
-    unsigned long long t_;                                                       \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-    __builtin_amdgcn_sched_barrier(0);                                           \
-    if (blockIdx.x == 0 && threadIdx.x == 0) g_pstamps[(k)] = t_;                \
+// every block's s_memrealtime (100 MHz, one clock for the whole device) at stamps 0, 1,
+// 8, 10, 11, 13: where the launch's tail comes from
+constexpr int PBLK_MAX = 8192, PBLK_N = 6;
+__device__ unsigned int g_pblk[PBLK_MAX * PBLK_N];
+__device__ __forceinline__ int pblk_slot(int k) {
+  return k == 0 ? 0 : k == 1 ? 1 : k == 8 ? 2 : k == 10 ? 3 : k == 11 ? 4 : k == 13 ? 5 : -1;
+}
+#define PST_DECL uint32_t pst_[14], pbt_[PBLK_N];
+#define PST(k)                                                                       \
+  do {                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    unsigned long long t_;                                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");     \
+    uint32_t v_;                                                                     \
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v_) : "s"((uint32_t)t_));                 \
+    if (pblk_slot(k) >= 0) {                                                         \
+      unsigned long long r_;                                                         \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r_)::"memory"); \
+      uint32_t w_;                                                                   \
+      asm volatile("v_mov_b32 %0, %1" : "=v"(w_) : "s"((uint32_t)r_));               \
+      pbt_[pblk_slot(k) < 0 ? 0 : pblk_slot(k)] = w_;                                \
+    }                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    pst_[(k)] = v_;                                                                  \
+  } while (0)
+#define PST_FLUSH()                                                                  \
+  do {                                                                               \
+    if (blockIdx.x == 0 && threadIdx.x == 0)                                         \
+      for (int k_ = 0; k_ < 14; ++k_) g_pstamps[k_] = pst_[k_];                      \
+    if (threadIdx.x == 0 && blockIdx.x < PBLK_MAX)                                   \
+      for (int k_ = 0; k_ < PBLK_N; ++k_) g_pblk[blockIdx.x * PBLK_N + k_] = pbt_[k_]; \
   } while (0)
 extern "C" int mapfx_partial_debug_stamps(unsigned long long* host_out) {
   return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_pstamps), sizeof(unsigned long long) * 16) ==
                  hipSuccess ? 0 : -1;
 }
+// n_blocks x 6 realtime stamps (diagnostic build)
+extern "C" int mapfx_partial_debug_blocks(unsigned int* host_out, int n_blocks) {
+  if (n_blocks < 0 || n_blocks > PBLK_MAX) return -1;
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_pblk), sizeof(unsigned int) * PBLK_N * n_blocks) ==
+                 hipSuccess ? 0 : -1;
+}
 #else
+#define PST_DECL
 #define PST(k) \
   do {         \
+  } while (0)
+#define PST_FLUSH() \
+  do {              \
   } while (0)
 #endif
 
@@ -81,6 +119,7 @@ struct PGeo {
   int gd32;                          // goal-distance tables are int32 (H * W > 32767), else int16
   int big;                           // workgroup-per-env path (N > 64 or H, W > 256), map in HBM
   int hs_log, wg_lds, huge_lds;      // its LDS hash size (log2), block LDS; huge-map BFS LDS
+  uint32_t m_wpr;                    // ceil(2^32 / wpr): wi / wpr = umulhi(wi, m_wpr) below rows * wpr
 };
 
 struct PArgs {
@@ -99,6 +138,7 @@ struct PArgs {
   const uint8_t* bits;
   const void* gd;  // int16 or int32 (g.gd32)
   int32_t* pdist;  // [E][N] goal distance of the current cell (carried), or NULL
+  int16_t* pnbr;   // [E][N][4] goal distances of its 4 neighbours (carried with pdist), or NULL
   const void* actions;
   int act_dtype;
   int do_step;       // 0: observe only
@@ -109,7 +149,6 @@ struct PArgs {
   float* state;
   uint8_t* avail;
   int32_t* err;
-  const double* sqrt_lut;   // sqrt(n), n = 0 .. sq_max
   const double* bonus_lut;  // (complete / gamma ** (limit - t)) * fac, t = 0 .. bonus_len-1
   // runner fusion (mapfx_partial_step_rows): observation rows go to obs_rows + e *
   // obs_env_stride (an EpisodeBatch time row) for the envs with obs_mask[e] != 0,
@@ -122,6 +161,11 @@ struct PArgs {
 };
 
 // where env e's observation rows go ([N][D] floats), or nullptr when not written
+// (partial_kernel: the caller has read obs_mask[e] with the launch's other loads)
+__device__ __forceinline__ float* obs_env_nomask(const PArgs& a, int e, int D, int N) {
+  if (a.obs_rows) return a.obs_rows + (long long)e * a.obs_env_stride;
+  return a.obs ? a.obs + (long long)e * N * D : nullptr;
+}
 __device__ __forceinline__ float* obs_env(const PArgs& a, int e, int D, int N) {
   if (a.obs_rows) return (a.obs_mask && !a.obs_mask[e]) ? nullptr : a.obs_rows + (long long)e * a.obs_env_stride;
   return a.obs ? a.obs + (long long)e * N * D : nullptr;
@@ -162,6 +206,78 @@ __device__ inline void wave_fence() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// sqrt(n) of a non-negative integer n <= sq_max in fp64 (math.sqrt of the reference's
+// squared distances): the device's correctly rounded sqrt, which mapfx_partial_create
+// checks bit for bit against host libm on all of 0 .. sq_max (it refuses the
+// configuration otherwise).  Computed, not loaded: a table load here would make every
+// later wait on the vector-memory counter also wait for the loads issued before it.
+__device__ __forceinline__ double isqrt_f64(int n) { return sqrt((double)n); }
+
+// the action (int64 as (lo, hi), int8 / int32 sign-extended into hi): 0..4, or -1 for
+// any value outside 0..4 (the env is then skipped, :174)
+__device__ __forceinline__ int act_decode(int lo, int hi) { return ((uint32_t)lo <= 4u && hi == 0) ? lo : -1; }
+// the action as the int64 the EpisodeBatch records
+__device__ __forceinline__ long long act_value(int lo, int hi) {
+  return (long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// Cross-lane sums inside an env's L-lane group without the LDS pipeline: DPP moves
+// within 16-lane rows (L <= 16: an env's lanes never leave their row), else shuffles.
+template <int CTRL>
+__device__ __forceinline__ int dpp_mov(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int group_sum(int x, int L) {
+  if (L == 16) {  // row_ror 8, 4, 2, 1
+    x += dpp_mov<0x128>(x);
+    x += dpp_mov<0x124>(x);
+    x += dpp_mov<0x122>(x);
+    return x + dpp_mov<0x121>(x);
+  }
+  if (L == 8) {  // quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror
+    x += dpp_mov<0xB1>(x);
+    x += dpp_mov<0x4E>(x);
+    return x + dpp_mov<0x141>(x);
+  }
+  if (L == 4) {
+    x += dpp_mov<0xB1>(x);
+    return x + dpp_mov<0x4E>(x);
+  }
+  if (L == 2) return x + dpp_mov<0xB1>(x);
+  if (L == 1) return x;
+  for (int o = 1; o < L; o <<= 1) x += __shfl_xor(x, o);
+  return x;
+}
+// `sum(rewards)` (:310): the naive left fold 0.0 + r[0] + r[1] + ... + r[N-1] in agent
+// order, valid in each env's agent-0 lane; r[k] arrives by a DPP row shift (lane i reads
+// lane i + k of its row), so L <= 16 (callers fold through LDS otherwise)
+template <int K>
+__device__ __forceinline__ double row_shl_f64(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const int lo = dpp_mov<0x100 + K>((int)(uint32_t)b);
+  const int hi = dpp_mov<0x100 + K>((int)(uint32_t)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+template <int K>
+__device__ __forceinline__ void fold_from(double& R, double x, int N) {
+  if constexpr (K < 16) {
+    if (K < N) R = R + row_shl_f64<K>(x);
+    fold_from<K + 1>(R, x, N);
+  }
+}
+__device__ __forceinline__ double row_fold(double x, int N) {
+  double R = 0.0 + x;
+  fold_from<1>(R, x, N);
+  return R;
+}
+
+// goal distance of neighbour `act` (0 up, 1 down, 2 left, 3 right) from the carried
+// pnbr entry (4 x int16 as two words)
+__device__ __forceinline__ int nbr_dist(uint2 nb, int act) {
+  const uint32_t w = act < 2 ? nb.x : nb.y;
+  return (int)(int16_t)(uint16_t)((act & 1) ? (w >> 16) : (w & 0xFFFFu));
 }
 
 // goal distance of cell `cell` in agent `oa`'s table (int16, or int32 when H * W > 32767:
@@ -669,7 +785,7 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
     if (!has[k]) continue;
     const int ag = tid + k * WG_THREADS;
     const int d0 = gr[k] - r[k], d1 = gc[k] - c[k];
-    const double nrm = a.sqrt_lut[d0 * d0 + d1 * d1];        // :937
+    const double nrm = isqrt_f64(d0 * d0 + d1 * d1);   // :937
     const double ux = nrm == 0.0 ? 0.0 : (double)d0 / nrm;   // :938-941
     const double uy = nrm == 0.0 ? 0.0 : (double)d1 / nrm;
     float* fr = feat + ag * FR;
@@ -727,7 +843,7 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
         const int sq = (int)(best >> 10);
         float* row = kn + sI * NF;
         for (int q = 0; q < 11; ++q) row[q] = feat[j * FR + q];
-        row[11] = (float)a.sqrt_lut[sq];
+        row[11] = (float)isqrt_f64(sq);
         row[12] = feat[j * FR + 11];
       }
       for (int sI = km1 + 1; sI < K; ++sI)
@@ -798,28 +914,106 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   int2* posL = (int2*)(lds + g.off_pos + cs * (64 * 8));
   double* rewL = (double*)(lds + g.off_rew + cs * g.rew_env_bytes);
 
+  PST_DECL
   PST(0);
   const long long oa = (long long)env * N + ag;
-  // ---- every global read of the launch issued up front, branch-free (idle lanes read
-  // entry 0 and ignore it), the bitmap's first words first: LDS staging then waits for
-  // them alone, the goal-distance lookups for the position and action alone, and the
-  // rest lands during the map build ----
+  // ---- every global read of the launch issued up front (idle lanes read entry 0),
+  // the bitmap's first words first; optional arrays behind uniform branches, and no
+  // loaded value used before the map build: a value tested right after its load would
+  // put a wait on the vector-memory counter (in-order: on every load before it) into
+  // the prologue ----
   const long long oc_ = has ? oa : 0;
   const int ec_ = env_ok ? env : 0;
+  const bool runner = a.do_step && a.ra.act_row != nullptr;
+  const bool post = a.ra.alive != nullptr;  // the runner's post pass, fused
+  const bool nb_carry = a.pnbr && a.pdist && !g.gd32;  // neighbour distances carried
   const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)ec_ * g.map_stride));
   const uint32_t bw0 = bsrc[ag < g.bits_words ? ag : 0];  // this lane's first bitmap word
+  // the step's action: one 8-byte load of the aligned block that holds it (whatever the
+  // dtype: the block lies in the element's page), decoded after the map build; the
+  // runner's address needs the env's row of the MAC output first
+  const int esh = a.act_dtype == MAPFX_I64 ? 3 : a.act_dtype == MAPFX_I32 ? 2 : 0;
+  int arow = 0;
+  long long ai = oc_;
+  if (runner) {
+    arow = a.ra.act_row[ec_];
+    ai = (has && arow >= 0) ? (long long)arow * a.ra.act_row_stride + ag : 0;
+  }
+  const uintptr_t abyte = (uintptr_t)(a.do_step ? a.actions : (const void*)a.pos) + ((uintptr_t)ai << esh);
+  const uint2 araw = *(const uint2*)(abyte & ~(uintptr_t)7);
   const int2 q = ((const int2*)a.goal)[oc_];
   const int2 ip = ((const int2*)a.init_pos)[oc_];
   const int2 p0 = ((const int2*)a.pos)[oc_];
-  int act = (a.do_step && has) ? step_action(a, env, ag, oa) : 4;  // the step's action
-  const int pd0 = a.pdist ? a.pdist[oc_] : PD_NONE;
+  int pd_raw = 0;
+  if (a.pdist) pd_raw = a.pdist[oc_];
+  uint2 nb0 = make_uint2(0u, 0u);
+  if (nb_carry && a.do_step) nb0 = ((const uint2*)a.pnbr)[oc_];
   const int steps0 = a.steps[oc_];
   const uint8_t at_goal0 = a.at_goal[oc_], dn0 = a.done[oc_], node0 = a.node[oc_];
   const int gcost0 = a.goal_cost[oc_], edge0 = a.edge[oc_];
   const int t0 = a.t[ec_], total0 = a.total_coll[ec_];
   const uint8_t term0 = a.terminated[ec_];
-  const bool reset_me = env_ok && a.do_reset && (!a.reset_mask || a.reset_mask[ec_]);
+  uint32_t om_raw = 1, rm_raw = 1, live_raw = 0;
+  if (a.obs_rows && a.obs_mask) om_raw = a.obs_mask[ec_];
+  if (a.do_reset && a.reset_mask) rm_raw = a.reset_mask[ec_];
+  double epr_raw = 0.0;
+  int64_t epl_raw = 0;
+  if (post) {
+    live_raw = a.ra.alive[ec_];
+    epr_raw = a.ra.ep_return[ec_];
+    epl_raw = a.ra.ep_length[ec_];
+  }
+  // ---- LDS map (c format) + dep map (obstacle flag in bit 7) ----
+  if (env_ok) {
+    if (ag < g.bits_words) bitsL[ag] = bw0;
+    for (int w = ag + g.L; w < g.bits_words; w += g.L) bitsL[w] = bsrc[w];  // maps past 16 x 32 words
+  }
+  PST(1);
+  wave_fence();
+  if (env_ok) {
+    // word wi of the padded map = row pr, cells 4 pw .. 4 pw + 3 (pr = wi / wpr by a
+    // multiply-high, exact below rows * wpr: checked at create); each word's 4 obstacle
+    // bits from the two bitmap words around its first cell, every read of a group of
+    // 4 words issued before any is used (no branch: off-grid cells are masked)
+    const int nw = g.rows * g.wpr;
+    for (int w0 = ag; w0 < nw; w0 += 4 * g.L) {
+      uint32_t blo[4], bhi[4], vm[4];
+      int sh[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int wi = w0 + u * g.L;
+        const int pr = (int)__umulhi((uint32_t)wi, g.m_wpr), pw = wi - pr * g.wpr;
+        const int rr = pr - g.P, cc = pw * 4 - g.pl;  // the word's grid row, first column
+        const bool rin = (unsigned)rr < (unsigned)g.H;
+        const int idx = (rin ? rr : 0) * g.W + cc;    // bit of the first cell (>= -8)
+        const int iw = idx >> 5;
+        blo[u] = bitsL[min(max(iw, 0), g.bits_words)];  // (bitsL has a slack word)
+        bhi[u] = bitsL[min(max(iw + 1, 0), g.bits_words)];
+        sh[u] = idx & 31;
+        const int lv = max(0, -cc), hv = min(4, max(0, g.W - cc));  // on-grid cells lv .. hv - 1
+        vm[u] = (rin && lv < hv) ? ((1u << hv) - 1u) & ~((1u << lv) - 1u) : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int wi = w0 + u * g.L;
+        if (wi < nw) {
+          const uint32_t b4 = (uint32_t)((((uint64_t)bhi[u] << 32) | blo[u]) >> sh[u]) & 0xFu;
+          const uint32_t ob4 = (b4 & vm[u]) | (~vm[u] & 0xFu);  // obstacle flags (off the grid: 1)
+          const uint32_t f = (ob4 * 0x00204081u) & 0x01010101u;  // bit j -> byte j
+          map32[wi] = f ^ 0x01010101u;  // c = 1 - obstacle before agents are added
+          dep32[wi] = (f << 7) | 0x7F7F7F7Fu;
+        }
+      }
+    }
+  }
+  wave_fence();
+  PST(2);
   // ---- state (:125-163 for a reset env) ----
+  const bool reset_me = env_ok && a.do_reset && rm_raw != 0;
+  const bool omask = om_raw != 0;
+  const uint8_t live0 = live_raw != 0 ? 1 : 0;
+  const double epr0 = epr_raw;
+  const int64_t epl0 = epl_raw;
   const int gr = q.x, gc = q.y, ir = ip.x, ic = ip.y;
   int r = 0, c = 0, steps = 0, gcost = -1, edge = 0;
   int pd = PD_NONE;  // goal distance of the current cell (carried)
@@ -835,57 +1029,47 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
       gcost = gcost0;
       node = node0;
       edge = edge0;
-      pd = pd0;
+      pd = a.pdist ? pd_raw : PD_NONE;  // (pd_raw is 0 without pdist)
     }
   }
-  if (act < 0 || act > 4) act = -1;
   int tcur = (env_ok && !reset_me) ? t0 : 0, total = (env_ok && !reset_me) ? total0 : 0;
   bool term = env_ok && !reset_me && term0 != 0;
-  // ---- LDS map (c format) + dep map (obstacle flag in bit 7) ----
-  if (env_ok) {
-    if (ag < g.bits_words) bitsL[ag] = bw0;
-    for (int w = ag + g.L; w < g.bits_words; w += g.L) bitsL[w] = bsrc[w];  // maps past 16 x 32 words
+  // the action (raw int64 as (alo, ahi); int8 / int32 sign-extended); an env outside
+  // the runner's bs stays
+  const uint32_t aw = (abyte & 4) ? araw.y : araw.x;
+  int alo, ahi;
+  if (a.act_dtype == MAPFX_I64) {
+    alo = (int)araw.x;
+    ahi = (int)araw.y;
+  } else if (a.act_dtype == MAPFX_I32) {
+    alo = (int)aw;
+    ahi = alo >> 31;
+  } else {
+    alo = (int)(int8_t)(uint8_t)(aw >> ((abyte & 3) * 8));
+    ahi = alo >> 31;
   }
-  // goal-path distances (:227-233): the move target's entry, speculatively (used when the
-  // agent moves), and the current cell's when no carried value applies -- issued here, so
-  // their latency overlaps the map build
-  PST(1);
+  int act = 4;
+  if (a.do_step && has && !(runner && arow < 0)) act = act_decode(alo, ahi);
+  // goal-path distances (:227-233): a moving agent's npd is its target's entry of the
+  // carried neighbour distances; without them (no pnbr, int32 tables, a state never reset)
+  // the target's table entry is looked up here, and the current cell's when no carried
+  // value applies (every non-step pass refreshes it)
+  const bool nb_ok = nb_carry && a.do_step && pd != PD_NONE;
   const bool need_cur = has && (!a.do_step || !a.pdist || pd == PD_NONE);
   int npd_t = 0;
-  if (has) {
+  if (has && !nb_ok) {
     const int tgt = (a.do_step && !dn) ? move_target(g, r, c, act) : -1;
     if (tgt >= 0) npd_t = goal_dist_at(g, a.gd, oa, tgt);
     if (need_cur) pd = goal_dist_at(g, a.gd, oa, r * g.W + c);
   }
-  wave_fence();
-  if (env_ok) {
-    for (int wi = ag; wi < g.rows * g.wpr; wi += g.L) {
-      const int pr = wi / g.wpr, pw = wi - pr * g.wpr;
-      const int rr = pr - g.P;
-      uint32_t f = 0x01010101u;  // obstacle flags of the word's 4 cells
-      if (rr >= 0 && rr < g.H) {
-        f = 0;
-        for (int j = 0; j < 4; ++j) {
-          const int cc = pw * 4 + j - g.pl;
-          uint32_t ob = 1;
-          if (cc >= 0 && cc < g.W) {
-            const int idx = rr * g.W + cc;
-            ob = (bitsL[idx >> 5] >> (idx & 31)) & 1u;
-          }
-          f |= ob << (8 * j);
-        }
-      }
-      map32[wi] = f ^ 0x01010101u;  // c = 1 - obstacle before agents are added
-      dep32[wi] = (f << 7) | 0x7F7F7F7Fu;
-    }
-  }
-  wave_fence();
+  PST(3);
   int cur = (r + g.P) * pitch + c + g.pl;
   if (has) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
   wave_fence();
+  PST(4);
 
-  PST(2);
   // ---- step (:165-310) ----
+  double Rsum = 0.0;  // sum(rewards) of the env (agent-0 lane)
   if (a.do_step && env_ok && !(PABL & 2)) {
     const bool skip = (__ballot(act < 0) & envmask) != 0;  // the reference asserts (:174)
     if (!skip) {
@@ -920,7 +1104,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
       }
       if (has) {                                            // :227-233
         const int opd = pd;
-        const int npd = moved ? npd_t : opd;
+        const int npd = moved ? (nb_ok ? nbr_dist(nb0, act) : npd_t) : opd;
         rew = rew + (double)(opd - npd) / (double)g.limit;
         pd = npd;
       }
@@ -932,6 +1116,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
         atomicAdd(&map32[nc >> 2], 1u << ((nc & 3) * 8));
       }
       wave_fence();
+      PST(5);
       const uint32_t dj = has ? dep[nc] : 0x7Fu;
       const uint32_t cn = has ? map[nc] : 0u;
       node = (has && cn + (dj >> 7) >= 3u) ? 1u : 0u;
@@ -949,8 +1134,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
         }
       }
       // env sums: total collisions += (sum(node) + sum(edge)) // 2  (:239)
-      int esum = has ? (int)node + edge : 0;
-      for (int o = 1; o < g.L; o <<= 1) esum += __shfl_xor(esum, o);
+      const int esum = group_sum(has ? (int)node + edge : 0, g.L);
       total += esum / 2;
       rew = rew + g.nc_rew * (double)node;  // :247
       rew = rew + g.ec_rew * (double)edge;  // :249
@@ -965,27 +1149,45 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
         const int bi = min(tcur, g.bonus_len - 1);
         rew = rew + a.bonus_lut[bi];
       }
+      PST(6);
       // sum(rewards): naive left fold in agent order (:310)
-      if (has) rewL[ag] = rew;
-      wave_fence();
-      if (ag == 0) {
-        double R = 0.0;
-        for (int j = 0; j < N; ++j) R = R + rewL[j];
-        if (a.reward) a.reward[env] = R;
+      if (g.L <= 16) {
+        const double R = row_fold(has ? rew : 0.0, N);
+        if (ag == 0) {
+          if (a.reward) a.reward[env] = R;
+          Rsum = R;
+        }
+      } else {
+        if (has) rewL[ag] = rew;
+        wave_fence();
+        if (ag == 0) {
+          double R = 0.0;
+          for (int j = 0; j < N; ++j) R = R + rewL[j];
+          if (a.reward) a.reward[env] = R;
+          Rsum = R;
+        }
       }
+      PST(7);
     } else {
       if (ag == 0 && a.err) atomicCAS(a.err, 0, env + 1);
       if (ag == 0 && a.reward) a.reward[env] = 0.0;
     }
   }
   wave_fence();
+  // the goal distances of the (new) cell's neighbours, carried to the next step: issued
+  // here, consumed before the staged copy-out (the observation rows hide their latency)
+  // -- unconditional loads (idle lanes read agent 0's table at (0, 0), an off-grid
+  // neighbour the cell itself; no branch, so no use of a value can move up to its load)
+  const int16_t* gt = (const int16_t*)a.gd + oc_ * g.hw + r * g.W + c;
+  const int nbd0 = gt[r > 0 ? -g.W : 0], nbd1 = gt[r + 1 < g.H ? g.W : 0];
+  const int nbd2 = gt[c > 0 ? -1 : 0], nbd3 = gt[c + 1 < g.W ? 1 : 0];
 
-  PST(3);
+  PST(8);
   // ---- observations of the current state (:312-391) ----
   // per-agent feature rows: curr, start, goal, unit vec, norm, node, edge, steps
   if (has) {
     const int d0 = gr - r, d1 = gc - c;
-    const double nrm = a.sqrt_lut[d0 * d0 + d1 * d1];        // :937
+    const double nrm = isqrt_f64(d0 * d0 + d1 * d1);   // :937
     const double ux = nrm == 0.0 ? 0.0 : (double)d0 / nrm;   // :938-941
     const double uy = nrm == 0.0 ? 0.0 : (double)d1 / nrm;
     float* fr = feat + ag * FR;
@@ -995,11 +1197,11 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
     posL[ag] = make_int2(r, c);
   }
   wave_fence();
-  PST(4);
+  PST(9);
   constexpr int WW = WIN * WIN;
   constexpr int DF = (KF > 0 && LF > 0) ? 2 * WW + NF * KF : 1;  // fast-path row length
   float o[DF];
-  float* const my_obs = env_ok ? obs_env(a, env, (KF > 0 && LF > 0) ? DF : g.D, N) : nullptr;
+  float* const my_obs = (env_ok && omask) ? obs_env_nomask(a, env, (KF > 0 && LF > 0) ? DF : g.D, N) : nullptr;
   if (has && my_obs && !(PABL & 1)) {
     float* kn;
     if constexpr (KF > 0 && LF > 0) {
@@ -1059,17 +1261,12 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
           const float* fj = feat + j * FR;
 #pragma unroll
           for (int q = 0; q < 11; ++q) row[q] = fj[q];
-          row[11] = (float)a.sqrt_lut[best >> 6];
+          row[11] = (float)isqrt_f64((int)(best >> 6));
           row[12] = fj[11];
         } else {
 #pragma unroll
           for (int q = 0; q < NF; ++q) row[q] = -1.0f;
         }
-      }
-      if (g.off_stage < 0) {  // rows straight to HBM (per-lane dword stores)
-        uint32_t* d = (uint32_t*)(my_obs + ag * D);
-#pragma unroll
-        for (int i = 0; i < D; ++i) d[i] = __float_as_uint(o[i]);
       }
     } else {
       // -------- generic path --------
@@ -1106,7 +1303,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
         const int sq = (int)(best >> 6);
         float* row = kn + sI * NF;
         for (int q = 0; q < 11; ++q) row[q] = feat[j * FR + q];
-        row[11] = (float)a.sqrt_lut[sq];
+        row[11] = (float)isqrt_f64(sq);
         row[12] = feat[j * FR + 11];
       }
       for (int sI = km1 + 1; sI < K; ++sI)
@@ -1114,8 +1311,17 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
     }
     (void)kn;
   }
-  PST(5);
+  PST(10);
+  // the carried neighbour distances (their loads have landed by now)
+  uint2 nb1 = make_uint2(((uint32_t)nbd0 & 0xFFFFu) | ((uint32_t)nbd1 << 16),
+                         ((uint32_t)nbd2 & 0xFFFFu) | ((uint32_t)nbd3 << 16));
+  asm volatile("" : "+v"(nb1.x), "+v"(nb1.y));
   if constexpr (KF > 0 && LF > 0) {
+    if (g.off_stage < 0 && has && my_obs && !(PABL & 1)) {  // rows straight to HBM (per-lane stores)
+      uint32_t* d = (uint32_t*)(my_obs + ag * DF);
+#pragma unroll
+      for (int i = 0; i < DF; ++i) d[i] = __float_as_uint(o[i]);
+    }
     // The rows of the envs of a staging group (the whole wave, or each half of it) are
     // one contiguous run of the destination (a.obs), or one run per env (EpisodeBatch
     // rows): stage each run in LDS as its byte image, at the run's own 16-byte
@@ -1190,20 +1396,19 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
       }
     }
   }
-  PST(6);
+  PST(11);
   (void)o;
   // avail (:399-433): neighbour in bounds and not a free-standing obstacle
-  if (has && a.avail) {
-    uint32_t m = 16u;
-    if (map[cur - pitch]) m |= 1u;
-    if (map[cur + pitch]) m |= 2u;
-    if (map[cur - 1]) m |= 4u;
-    if (map[cur + 1]) m |= 8u;
-    a.avail[oa] = (uint8_t)m;
+  uint32_t am = 16u;
+  if (has && (a.avail || a.ra.ep_avail)) {
+    if (map[cur - pitch]) am |= 1u;
+    if (map[cur + pitch]) am |= 2u;
+    if (map[cur - 1]) am |= 4u;
+    if (map[cur + 1]) am |= 8u;
+    if (a.avail) a.avail[oa] = (uint8_t)am;
   }
   // state (:377-387): [total collisions, step count, sum(each goal cost)]
-  int gsum = has ? gcost : 0;
-  for (int o = 1; o < g.L; o <<= 1) gsum += __shfl_xor(gsum, o);
+  const int gsum = group_sum(has ? gcost : 0, g.L);
   if (env_ok && ag == 0 && a.state) {
     a.state[3 * env + 0] = (float)total;
     a.state[3 * env + 1] = (float)tcur;
@@ -1219,29 +1424,76 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
     a.node[oa] = (uint8_t)node;
     a.edge[oa] = edge;
     if (a.pdist) a.pdist[oa] = pd;
+    if (nb_carry) ((uint2*)a.pnbr)[oa] = nb1;
+    if (runner && arow >= 0) {  // the EpisodeBatch's actions / actions_onehot rows at ts
+      const long long v = act_value(alo, ahi);
+      if (a.ra.ep_actions)
+        a.ra.ep_actions[(long long)env * a.ra.ep_actions_sb + (long long)a.ra.ts * a.ra.ep_actions_st + ag] = v;
+      if (a.ra.ep_onehot) {
+        float* oh = a.ra.ep_onehot + (long long)env * a.ra.ep_onehot_sb +
+                    (long long)a.ra.ts * a.ra.ep_onehot_st + (long long)ag * 5;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) oh[k] = v == k ? 1.0f : 0.0f;
+      }
+    }
   }
   if (env_ok && ag == 0) {
     a.t[env] = tcur;
     a.terminated[env] = term ? 1 : 0;
     a.total_coll[env] = total;
   }
-  PST(7);
+  if (post && env_ok) {  // runner_post_kernel (runner.hip) for a running env, fused
+    const mapfx_runner_acts& ra = a.ra;
+    if (live0) {
+      if (ag == 0) {
+        if (ra.ep_reward) ra.ep_reward[(long long)env * ra.ep_reward_sb + (long long)ra.ts * ra.ep_reward_st] = (float)Rsum;
+        // env_terminated = terminated and not info.get("episode_limit") (parallel_runner.py:146-150):
+        // MARL_PARTIAL's info has no "episode_limit" key
+        if (ra.ep_term) ra.ep_term[(long long)env * ra.ep_term_sb + (long long)ra.ts * ra.ep_term_st] = term ? 1 : 0;
+        ra.ep_return[env] = epr0 + Rsum;
+        ra.ep_length[env] = epl0 + 1;
+        ra.alive[env] = term ? 0 : 1;
+        if (ra.ep_state) {  // update(pre_transition_data, bs, ts + 1): state, avail, filled
+          float* d = ra.ep_state + (long long)env * ra.ep_state_sb;
+          d[0] = (float)total;
+          d[1] = (float)tcur;
+          d[2] = (float)gsum;
+        }
+        if (ra.ep_filled) ra.ep_filled[(long long)env * ra.ep_filled_sb] = 1;
+      }
+      if (has && ra.ep_avail) {
+        int32_t* d = ra.ep_avail + (long long)env * ra.ep_avail_sb + ag * 5;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) d[k] = (int32_t)((am >> k) & 1u);
+      }
+    }
+    if (ag == 0) ra.alive_prev[env] = live0;
+  }
+  PST(12);
 #ifdef PARTIAL_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
-  PST(8);
+  PST(13);
+  PST_FLUSH();
 #endif
 }
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// sqrt(i), i = 0 .. n, with the same device sqrt isqrt_f64 uses (mapfx_partial_create
+// compares it bit for bit with host libm before the kernels may use it)
+__global__ void __launch_bounds__(256) sqrt_probe_kernel(double* out, int n) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i <= n) out[i] = sqrt((double)i);
+}
 
 }  // namespace
 
 struct mapfx_partial_t {
   mapfx_partial_cfg cfg;
   PGeo geo;
-  double* sqrt_lut;
   double* bonus_lut;
   int device;
+  int no_nbcarry;  // diagnostic / A-B (MAPFX_PARTIAL_NBCARRY=0): ignore the state's pnbr
 };
 
 namespace {
@@ -1291,8 +1543,8 @@ int wg_apl(const PGeo& g) { return (g.N + WG_THREADS - 1) / WG_THREADS; }
 int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
   const PGeo& g = h->geo;
   if (g.E == 0) return MAPFX_OK;
-  a.sqrt_lut = h->sqrt_lut;
   a.bonus_lut = h->bonus_lut;
+  if (h->no_nbcarry) a.pnbr = nullptr;
   if (g.big) {  // N > 64 or a side > 256: one workgroup per env, map in HBM
     void (*fn)(PGeo, PArgs) = pick_wg(g.win, wg_apl(g));
     if (!fn) return perr(MAPFX_EINVAL, "obs_window must be one of 0, 1, 3, 5, 7, 9");
@@ -1335,6 +1587,7 @@ void fill_state(PArgs& a, const mapfx_partial_state* st) {
   a.bits = st->map_bits;
   a.gd = st->goal_dist;
   a.pdist = st->pdist;
+  a.pnbr = st->pnbr;
 }
 
 void fill_out(PArgs& a, const mapfx_partial_out* o) {
@@ -1365,8 +1618,9 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   mapfx_partial_t* h = new (std::nothrow) mapfx_partial_t();
   if (!h) return perr(MAPFX_ENOMEM, "host allocation failed");
   h->cfg = c;
-  h->sqrt_lut = nullptr;
   h->bonus_lut = nullptr;
+  h->no_nbcarry = 0;
+  if (const char* ev = getenv("MAPFX_PARTIAL_NBCARRY")) h->no_nbcarry = atoi(ev) == 0;
   if (hipGetDevice(&h->device) != hipSuccess) h->device = 0;
   PGeo& g = h->geo;
   memset(&g, 0, sizeof(g));
@@ -1388,6 +1642,7 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.pitch = round_up(g.pl + c.W + g.P, 4);
   g.rows = c.H + 2 * g.P;
   g.wpr = g.pitch / 4;
+  g.m_wpr = (uint32_t)((0x100000000ull + (unsigned long long)g.wpr - 1ull) / (unsigned long long)g.wpr);
   g.bits_words = (c.H * c.W + 31) / 32;
   g.map_shared = c.map_shared ? 1 : 0;
   g.map_stride = mapfx_map_stride(c.H, c.W);
@@ -1504,7 +1759,16 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
       return rc0;
     }
   }
-  // LUTs from the host libm (math.sqrt, float ** int): correctly rounded references
+  {  // the map build's multiply-high division (partial_kernel) must be exact on its range
+    const unsigned long long nw = (unsigned long long)g.rows * g.wpr;
+    for (unsigned long long wi = 0; wi < nw; ++wi)
+      if (((wi * g.m_wpr) >> 32) != wi / (unsigned long long)g.wpr) {
+        delete h;
+        return perr(MAPFX_EINVAL, "MARL_PARTIAL: map too large for the padded-map word index");
+      }
+  }
+  // the completion-bonus LUT from host libm (float ** int is correctly rounded there) and
+  // the sqrt reference values the device sqrt is checked against
   const int S = std::max(c.H, c.W);
   g.sq_max = 2 * (S - 1) * (S - 1);
   g.bonus_len = c.episode_limit + BONUS_EXTRA;
@@ -1521,10 +1785,22 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   for (int i = 0; i <= g.sq_max; ++i) sq[i] = libm_sqrt((double)i);
   for (int t = 0; t < g.bonus_len; ++t)  // (complete / (gamma ** (limit - t))) * fac  (:292)
     bo[t] = (c.complete_reward / libm_pow(c.gamma, (double)(c.episode_limit - t))) * c.complete_fac;
-  int rc = check_hip(hipMalloc(&h->sqrt_lut, sizeof(double) * (g.sq_max + 1)), "hipMalloc");
-  if (!rc) rc = check_hip(hipMalloc(&h->bonus_lut, sizeof(double) * g.bonus_len), "hipMalloc");
-  if (!rc) rc = check_hip(hipMemcpy(h->sqrt_lut, sq, sizeof(double) * (g.sq_max + 1), hipMemcpyHostToDevice), "hipMemcpy");
+  int rc = check_hip(hipMalloc(&h->bonus_lut, sizeof(double) * g.bonus_len), "hipMalloc");
   if (!rc) rc = check_hip(hipMemcpy(h->bonus_lut, bo, sizeof(double) * g.bonus_len, hipMemcpyHostToDevice), "hipMemcpy");
+  // the kernels' sqrt (isqrt_f64) must equal host libm on every argument they can use
+  double* probe = nullptr;
+  double* back = rc ? nullptr : (double*)malloc(sizeof(double) * (g.sq_max + 1));
+  if (!rc && !back) rc = perr(MAPFX_ENOMEM, "host allocation failed");
+  if (!rc) rc = check_hip(hipMalloc(&probe, sizeof(double) * (g.sq_max + 1)), "hipMalloc");
+  if (!rc) {
+    hipLaunchKernelGGL(sqrt_probe_kernel, dim3((unsigned)(g.sq_max / 256 + 1)), dim3(256), 0, 0, probe, g.sq_max);
+    rc = check_hip(hipGetLastError(), "sqrt_probe_kernel launch");
+  }
+  if (!rc) rc = check_hip(hipMemcpy(back, probe, sizeof(double) * (g.sq_max + 1), hipMemcpyDeviceToHost), "hipMemcpy");
+  if (!rc && memcmp(back, sq, sizeof(double) * (g.sq_max + 1)) != 0)
+    rc = perr(MAPFX_EINVAL, "MARL_PARTIAL: the device fp64 sqrt differs from host libm (observations would not match)");
+  if (probe) (void)hipFree(probe);
+  free(back);
   free(sq);
   free(bo);
   if (rc) {
@@ -1537,7 +1813,6 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
 
 void mapfx_partial_destroy(mapfx_partial_t* h) {
   if (!h) return;
-  if (h->sqrt_lut) (void)hipFree(h->sqrt_lut);
   if (h->bonus_lut) (void)hipFree(h->bonus_lut);
   delete h;
 }
@@ -1638,6 +1913,8 @@ int mapfx_partial_step_rows(mapfx_partial_t* h, const mapfx_partial_state* st, c
   a.do_step = 1;
   return launch(h, a, stream);
 }
+
+int mapfx_partial_fuses_post(const mapfx_partial_t* h) { return h && !h->geo.big ? 1 : 0; }
 
 int mapfx_partial_step_runner(mapfx_partial_t* h, const mapfx_partial_state* st, const void* actions,
                               int action_dtype, const mapfx_runner_acts* ra, const mapfx_partial_out* out,

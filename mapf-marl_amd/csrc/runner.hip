@@ -272,10 +272,36 @@ int mapfx_runner_step(mapfx_partial_t* h, const mapfx_partial_state* st, const m
   ra.ep_onehot_sb = rows->onehot_sb;
   ra.ep_onehot_st = rows->onehot_st;
   ra.ts = ts;
-  float* obs_row = rows->obs && ts + 1 < rows->max_t ? rows->obs + (int64_t)(ts + 1) * rows->obs_st : nullptr;
+  const bool nxt = ts + 1 < rows->max_t;
+  // the post pass in the env step's write-back too (the one-wave-per-env-group kernel):
+  // then only the compaction runs after it
+  const bool fpost = mapfx_partial_fuses_post(h) != 0;
+  if (fpost) {
+    ra.alive = rs->alive;
+    ra.alive_prev = rs->alive_prev;
+    ra.ep_return = rs->ep_return;
+    ra.ep_length = rs->ep_length;
+    ra.ep_reward = rows->reward;
+    ra.ep_reward_sb = rows->reward_sb;
+    ra.ep_reward_st = rows->reward_st;
+    ra.ep_term = rows->terminated;
+    ra.ep_term_sb = rows->terminated_sb;
+    ra.ep_term_st = rows->terminated_st;
+    ra.ep_state = nxt && rows->state ? rows->state + (int64_t)(ts + 1) * rows->state_st : nullptr;
+    ra.ep_state_sb = rows->state_sb;
+    ra.ep_avail = nxt && rows->avail ? rows->avail + (int64_t)(ts + 1) * rows->avail_st : nullptr;
+    ra.ep_avail_sb = rows->avail_sb;
+    ra.ep_filled = nxt && rows->filled ? rows->filled + (int64_t)(ts + 1) * rows->filled_st : nullptr;
+    ra.ep_filled_sb = rows->filled_sb;
+  }
+  float* obs_row = rows->obs && nxt ? rows->obs + (int64_t)(ts + 1) * rows->obs_st : nullptr;
   if ((rc = mapfx_partial_step_runner(h, st, actions, action_dtype, &ra, out, obs_row, rows->obs_sb,
                                       rs->alive, stream)))
     return rc;
+  if (fpost) {
+    hipLaunchKernelGGL(runner_compact_kernel, dim3(1), dim3(CT), 0, (hipStream_t)stream, *rs, counts_out);
+    return launch_ok("runner_compact_kernel launch");
+  }
   if (!rows->obs) return mapfx_runner_post(rs, st->terminated, out, ts, counts_out, rows, stream);
   mapfx_episode_rows r2 = *rows;
   r2.obs = nullptr;

@@ -63,7 +63,7 @@ class PCfg(ctypes.Structure):  # include/mapfx_partial.h
 class PState(ctypes.Structure):
     _fields_ = [(k, c_vp) for k in ("pos", "goal", "init_pos", "steps", "at_goal", "done",
                                     "goal_cost", "node", "edge", "t", "terminated", "total_coll",
-                                    "map_bits", "goal_dist", "pdist")]
+                                    "map_bits", "goal_dist", "pdist", "pnbr")]
 
 
 class POut(ctypes.Structure):
@@ -111,7 +111,7 @@ class RState(ctypes.Structure):  # include/mapfx_runner.h mapfx_runner_state
                             "env_steps", "env_actions", "bs_inv")]
 
 
-ABI_VERSION = 3  # include/mapfx.h MAPFX_ABI_VERSION
+ABI_VERSION = 4  # include/mapfx.h MAPFX_ABI_VERSION
 
 
 class MapfxError(RuntimeError):

@@ -116,13 +116,17 @@ class MarlPartialBatch:
         gd_dt = torch.int32 if lib.mapfx_partial_goal_dist_elem_size(self.H, self.W) == 4 \
             else torch.int16
         self.goal_dist = z((E, N, self.H * self.W), gd_dt)
+        # the goal distances of each agent's 4 neighbour cells, carried with pdist (int16
+        # tables only): a step reads a moving agent's npd from it
+        self.pnbr = z((E, N, 4), torch.int16) if gd_dt == torch.int16 else None
         self.out = {k: v[k] for k in ("reward", "obs", "state", "avail")}
         self._state = _abi.PState(
             pos=ptr(self.pos), goal=ptr(self.goal), init_pos=ptr(self.init_pos),
             steps=ptr(self.steps), at_goal=ptr(self.at_goal), done=ptr(self.done),
             goal_cost=ptr(self.goal_cost), node=ptr(self.node), edge=ptr(self.edge), t=ptr(self.t),
             terminated=ptr(self.terminated), total_coll=ptr(self.total_coll),
-            map_bits=ptr(self.bits), goal_dist=ptr(self.goal_dist), pdist=ptr(self.pdist))
+            map_bits=ptr(self.bits), goal_dist=ptr(self.goal_dist), pdist=ptr(self.pdist),
+            pnbr=ptr(self.pnbr) if self.pnbr is not None else None)
         self._out = _abi.POut(reward=ptr(self.out["reward"]), obs=ptr(self.out["obs"]),
                               state=ptr(self.out["state"]), avail=ptr(self.out["avail"]),
                               err=ptr(self.err))

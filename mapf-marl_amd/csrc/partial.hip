@@ -47,7 +47,7 @@
 // in registers until the end (PST_FLUSH): a store per stamp would make the kernel's
 // waits on the vector-memory counter wait for it too.
 __device__ unsigned long long g_pstamps[16];
-// every block's s_memrealtime (100 MHz, one clock for the whole device) at stamps 0, 1,
+// every wave's s_memrealtime (100 MHz, one clock for the whole device) at stamps 0, 1,
 // 8, 10, 11, 13: where the launch's tail comes from
 constexpr int PBLK_MAX = 8192, PBLK_N = 6;
 __device__ unsigned int g_pblk[PBLK_MAX * PBLK_N];
@@ -76,8 +76,8 @@ __device__ __forceinline__ int pblk_slot(int k) {
   do {                                                                               \
     if (blockIdx.x == 0 && threadIdx.x == 0)                                         \
       for (int k_ = 0; k_ < 14; ++k_) g_pstamps[k_] = pst_[k_];                      \
-    if (threadIdx.x == 0 && blockIdx.x < PBLK_MAX)                                   \
-      for (int k_ = 0; k_ < PBLK_N; ++k_) g_pblk[blockIdx.x * PBLK_N + k_] = pbt_[k_]; \
+    if (lane64 == 0 && gw < PBLK_MAX)                                                \
+      for (int k_ = 0; k_ < PBLK_N; ++k_) g_pblk[gw * PBLK_N + k_] = pbt_[k_];         \
   } while (0)
 extern "C" int mapfx_partial_debug_stamps(unsigned long long* host_out) {
   return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_pstamps), sizeof(unsigned long long) * 16) ==
@@ -104,6 +104,7 @@ namespace {
 constexpr int NF = 13;   // KNN features per agent (:81)
 constexpr int FR = 12;   // per-agent feature row in LDS (all but the pairwise distance)
 constexpr int BONUS_EXTRA = 65536;  // completion-bonus LUT entries past the episode limit
+constexpr int PARTIAL_MAX_WPB = 4;  // partial_kernel: waves per block (g.wpb <= this)
 
 struct PGeo {
   int H, W, N, E;
@@ -111,7 +112,7 @@ struct PGeo {
   int P, pl, pitch, rows, wpr;       // padded LDS map
   int bits_words, map_shared;
   long long map_stride;
-  int map_env_bytes, bits_env_bytes, feat_env_bytes, rew_env_bytes, stage_env_bytes, stage_lanes;
+  int map_env_bytes, bits_env_bytes, feat_env_bytes, pos_env_bytes, rew_env_bytes, stage_env_bytes, stage_lanes;
   int off_map, off_dep, off_bits, off_feat, off_pos, off_rew, off_stage, lds;  // off_stage < 0: none
   int win, K, D, limit, hw;          // window, knn, obs dim, episode limit, H*W
   double move_rew, stay_rew, stay_goal_rew, nc_rew, ec_rew, env_rew;
@@ -120,6 +121,7 @@ struct PGeo {
   int big;                           // workgroup-per-env path (N > 64 or H, W > 256), map in HBM
   int hs_log, wg_lds, huge_lds;      // its LDS hash size (log2), block LDS; huge-map BFS LDS
   uint32_t m_wpr;                    // ceil(2^32 / wpr): wi / wpr = umulhi(wi, m_wpr) below rows * wpr
+  int wpb;                           // partial_kernel: waves per block (each with g.lds of LDS)
 };
 
 struct PArgs {
@@ -265,6 +267,16 @@ __device__ __forceinline__ void fold_from(double& R, double x, int N) {
   if constexpr (K < 16) {
     if (K < N) R = R + row_shl_f64<K>(x);
     fold_from<K + 1>(R, x, N);
+  }
+}
+// edge collisions against every other lane of a 16-lane row (lane i sees lane (i + k) % 16
+// for k = 1..15; lanes past N hold an unmoved cell and never match a moving agent)
+template <int K>
+__device__ __forceinline__ void dpp_edge_scan(int cur, int nc, int& e) {
+  if constexpr (K < 16) {
+    const int oj = dpp_mov<0x120 + K>(cur), nj = dpp_mov<0x120 + K>(nc);
+    e += (oj == nc) & (nj == cur);
+    dpp_edge_scan<K + 1>(cur, nc, e);
   }
 }
 __device__ __forceinline__ double row_fold(double x, int N) {
@@ -889,15 +901,20 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
 // Step / observe / reset kernel (one launch = one env step or observation pass).
 // ---------------------------------------------------------------------------
 // KF / LF: K and lanes-per-env fixed at compile time (0: run-time generic path)
+// A block is g.wpb independent waves (no barrier between them): bigger blocks let the
+// dispatcher start the launch's waves sooner (one wave per block took ~1.4 us to have
+// all 1024 waves of the bench shape running).
 template <int WIN, int KF, int LF>
-__global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
-  extern __shared__ __align__(16) unsigned char lds[];
+__global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, PArgs a) {
+  extern __shared__ __align__(16) unsigned char lds_blk[];
   constexpr int H2 = WIN / 2;
-  const int lane64 = threadIdx.x;
+  const int lane64 = threadIdx.x & 63;
+  const int gw = (int)blockIdx.x * g.wpb + (int)(threadIdx.x >> 6);  // this wave's index
+  unsigned char* const lds = lds_blk + (threadIdx.x >> 6) * g.lds;
   const int slot = lane64 >> g.lshift;
   const int ag = lane64 & (g.L - 1);
   const int base = slot << g.lshift;
-  const int env = blockIdx.x * g.EPW + slot;
+  const int env = gw * g.EPW + slot;
   const int N = g.N;
   const bool env_ok = slot < g.EPW && env < g.E;
   const bool has = env_ok && ag < N;
@@ -911,7 +928,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   uint32_t* dep32 = (uint32_t*)dep;
   uint32_t* bitsL = (uint32_t*)(lds + g.off_bits + cs * g.bits_env_bytes);
   float* feat = (float*)(lds + g.off_feat + cs * g.feat_env_bytes);
-  int2* posL = (int2*)(lds + g.off_pos + cs * (64 * 8));
+  int2* posL = (int2*)(lds + g.off_pos + cs * g.pos_env_bytes);
   double* rewL = (double*)(lds + g.off_rew + cs * g.rew_env_bytes);
 
   PST_DECL
@@ -1125,11 +1142,17 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
       const bool suspect = moved && pre > 0;
       if (__ballot(suspect)) {
         if (suspect && pre == 1) edge = (dj & 0x7Fu) == (uint32_t)(act ^ 1) ? 1 : 0;
-        if (__ballot(suspect && pre > 1)) {
-          for (int j = 0; j < N; ++j) {
-            const int oj = __shfl(cur, base + j);
-            const int nj = __shfl(nc, base + j);
-            if (suspect && pre > 1) edge += (oj == nc) & (nj == cur);
+        if (__ballot(suspect && pre > 1)) {  // stacked pre-occupants: scan the env's agents
+          if (g.L == 16) {  // the env is one DPP row: rotate its (old, new) cells past each lane
+            int e2 = 0;
+            dpp_edge_scan<1>(cur, nc, e2);
+            if (suspect && pre > 1) edge += e2;
+          } else {
+            for (int j = 0; j < N; ++j) {
+              const int oj = __shfl(cur, base + j);
+              const int nj = __shfl(nc, base + j);
+              if (suspect && pre > 1) edge += (oj == nc) & (nj == cur);
+            }
           }
         }
       }
@@ -1202,11 +1225,79 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
   constexpr int DF = (KF > 0 && LF > 0) ? 2 * WW + NF * KF : 1;  // fast-path row length
   float o[DF];
   float* const my_obs = (env_ok && omask) ? obs_env_nomask(a, env, (KF > 0 && LF > 0) ? DF : g.D, N) : nullptr;
+  // Staged copy-out (fast path): the rows of the envs of a staging group (the whole wave,
+  // or each half of it) are one contiguous run of the destination (a.obs), or one run
+  // per env (EpisodeBatch rows): each run is staged in LDS as its byte image, at the
+  // run's own 16-byte misalignment, and copied with lane-contiguous 16-byte stores --
+  // per-lane dword stores of 460-byte rows touch 64 lines each.  The images alias the LDS
+  // regions the step is done with (dep onwards).  (Sending the window planes first, while
+  // the K-nearest rows are built, measured 19.0 vs 15.2 us: chunks of partial lines.)
+  constexpr bool FAST = KF > 0 && LF > 0;
+  const bool one_run = a.obs_rows == nullptr;
+  const bool staged = FAST && (a.obs || a.obs_rows) && g.off_stage >= 0 && !(PABL & 4);
+  // this lane's row of group gi's image (G lanes per group)
+  auto stage_row = [&](int gi, int G, int i0, int i1) {
+    const int s0 = (G * gi) >> g.lshift;
+    if (has && my_obs && lane64 / G == gi) {
+      const int kme = slot - s0;  // this lane's env within the group
+      const float* rb = one_run ? a.obs + (long long)(gw * g.EPW + s0) * N * DF : my_obs;
+      const uint32_t mis = (uint32_t)(uintptr_t)rb & 15u;
+      const int k = one_run ? 0 : kme;
+      const int ri = (one_run ? kme * N : 0) + ag;  // row within the run
+      uint32_t* row = (uint32_t*)(lds + g.off_stage + k * g.stage_env_bytes + mis + ri * (DF * 4));
+#pragma unroll
+      for (int i = 0; i < DF; ++i)
+        if (i >= i0 && i < i1) row[i] = __float_as_uint(o[i]);
+    }
+  };
+  // copy group gi's runs
+  auto copy_runs = [&](int gi, int G) {
+    const int s0 = (G * gi) >> g.lshift;
+    const int ne = max(0, min(min(G >> g.lshift, g.EPW - s0), g.E - (gw * g.EPW + s0)));  // signed
+    const int nrun = one_run ? (ne > 0 ? 1 : 0) : ne;
+    const int rowB = DF * 4;
+    for (int k = 0; k < nrun; ++k) {
+      unsigned char* gdst;
+      if (one_run) {
+        gdst = (unsigned char*)(a.obs + (long long)(gw * g.EPW + s0) * N * DF);
+      } else {  // env s0 + k's destination, from its agent-0 lane (NULL: masked)
+        const uint64_t pe = (uint64_t)(uintptr_t)my_obs;
+        const int src = (s0 + k) << g.lshift;
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)pe, src);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(pe >> 32), src);
+        gdst = (unsigned char*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+        if (!gdst) continue;
+      }
+      const uint32_t mis = (uint32_t)(uintptr_t)gdst & 15u;
+      const unsigned char* img = lds + g.off_stage + k * g.stage_env_bytes + mis;
+      const int nbytes = (one_run ? ne : 1) * N * rowB;
+      const int head = mis ? min(16 - (int)mis, nbytes) : 0;  // a multiple of 4
+      const int body = (nbytes - head) & ~15;
+      if (lane64 < head / 4) ((uint32_t*)gdst)[lane64] = ((const uint32_t*)img)[lane64];
+      const uint4* s4 = (const uint4*)(img + head);  // 16-byte aligned: mis + head
+      uint4* g4 = (uint4*)(gdst + head);
+      const int n16 = body / 16;
+      // four LDS reads in flight per lane before their stores
+      for (int i = lane64; i < n16; i += 256) {
+        const bool b1 = i + 64 < n16, b2 = i + 128 < n16, b3 = i + 192 < n16;
+        const uint4 v0 = s4[i];
+        uint4 v1, v2, v3;
+        if (b1) v1 = s4[i + 64];
+        if (b2) v2 = s4[i + 128];
+        if (b3) v3 = s4[i + 192];
+        g4[i] = v0;
+        if (b1) g4[i + 64] = v1;
+        if (b2) g4[i + 128] = v2;
+        if (b3) g4[i + 192] = v3;
+      }
+      const int tail = nbytes - head - body;
+      if (lane64 < tail / 4)
+        ((uint32_t*)(gdst + head + body))[lane64] = ((const uint32_t*)(img + head + body))[lane64];
+    }
+  };
   if (has && my_obs && !(PABL & 1)) {
-    float* kn;
-    if constexpr (KF > 0 && LF > 0) {
+    if constexpr (FAST) {
       // -------- fast path: the whole row in registers --------
-      constexpr int D = DF;
       if constexpr (WIN > 0) {  // window planes (:327-342) from whole map words
         const int wb = (cur - H2 * pitch - H2);
         const int sh = (wb & 3) * 8;
@@ -1245,6 +1336,8 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
       k0[12] = me[11];
       uint32_t prev = 0u;
       bool first = true;
+      // (a branch per round measured faster than computing every round and selecting -1:
+      // 15.2 vs 16.2 us)
 #pragma unroll
       for (int sI = 1; sI < KF; ++sI) {
         float* row = o + 2 * WW + sI * NF;
@@ -1282,7 +1375,7 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
       }
       // K nearest agents (:346-372): self first, then the k-1 nearest others by L2
       // distance (sorted() is stable: ties by agent index); rows past min(N, K) = -1
-      kn = o + 2 * WW;
+      float* kn = o + 2 * WW;
       const int K = g.K;
       const int km1 = min(N, K) - 1;
       for (int q = 0; q < 11; ++q) kn[q] = feat[ag * FR + q];
@@ -1309,89 +1402,28 @@ __global__ void __launch_bounds__(64) partial_kernel(PGeo g, PArgs a) {
       for (int sI = km1 + 1; sI < K; ++sI)
         for (int q = 0; q < NF; ++q) kn[sI * NF + q] = -1.0f;
     }
-    (void)kn;
   }
   PST(10);
   // the carried neighbour distances (their loads have landed by now)
   uint2 nb1 = make_uint2(((uint32_t)nbd0 & 0xFFFFu) | ((uint32_t)nbd1 << 16),
                          ((uint32_t)nbd2 & 0xFFFFu) | ((uint32_t)nbd3 << 16));
   asm volatile("" : "+v"(nb1.x), "+v"(nb1.y));
-  if constexpr (KF > 0 && LF > 0) {
+  if constexpr (FAST) {
     if (g.off_stage < 0 && has && my_obs && !(PABL & 1)) {  // rows straight to HBM (per-lane stores)
       uint32_t* d = (uint32_t*)(my_obs + ag * DF);
 #pragma unroll
       for (int i = 0; i < DF; ++i) d[i] = __float_as_uint(o[i]);
     }
-    // The rows of the envs of a staging group (the whole wave, or each half of it) are
-    // one contiguous run of the destination (a.obs), or one run per env (EpisodeBatch
-    // rows): stage each run in LDS as its byte image, at the run's own 16-byte
-    // misalignment, and copy it with lane-contiguous 16-byte stores -- per-lane dword
-    // stores of 460-byte rows touch 64 lines each.  The images alias the LDS regions
-    // the step and the observation rows are done with (dep onwards; the rows are in
-    // registers by now).
-    if ((a.obs || a.obs_rows) && g.off_stage >= 0 && !(PABL & 4)) {
-      constexpr int D = DF;
-      const int G = g.stage_lanes;       // 64 or 32
-      const int SE = g.stage_env_bytes;  // one env's rows + 16 bytes of alignment slack
-      const int blk = (int)blockIdx.x;   // (unsigned blockIdx would make g.E - ... unsigned)
-      const bool one_run = a.obs_rows == nullptr;
-      const int run_bytes = N * D * 4;
+    if (staged) {
+      const int G = g.stage_lanes;  // 64 or 32
       wave_fence();
       for (int gi = 0; gi < 64 / G; ++gi) {
-        // envs of this group: slots s0 .. s0 + ne - 1
-        const int s0 = (G * gi) >> g.lshift;
-        const int ne = max(0, min(min(G >> g.lshift, g.EPW - s0), g.E - (blk * g.EPW + s0)));  // signed
-        if (ne == 0) break;
-        if (has && my_obs && lane64 / G == gi) {
-          const int kme = slot - s0;  // this lane's env within the group
-          const float* rb = one_run ? a.obs + (long long)(blk * g.EPW + s0) * N * D : my_obs;
-          const uint32_t mis = (uint32_t)(uintptr_t)rb & 15u;
-          const int k = one_run ? 0 : kme;
-          const int ri = (one_run ? kme * N : 0) + ag;  // row within the run
-          uint32_t* row = (uint32_t*)(lds + g.off_stage + k * SE + mis + ri * (D * 4));
-#pragma unroll
-          for (int i = 0; i < D; ++i) row[i] = __float_as_uint(o[i]);
-        }
+        if (max(0, min(min(G >> g.lshift, g.EPW - ((G * gi) >> g.lshift)),
+                       g.E - (gw * g.EPW + ((G * gi) >> g.lshift)))) == 0)
+          break;
+        stage_row(gi, G, 0, DF);
         wave_fence();
-        const int nrun = one_run ? 1 : ne;
-        for (int k = 0; k < nrun; ++k) {
-          unsigned char* gdst;
-          if (one_run) {
-            gdst = (unsigned char*)(a.obs + (long long)(blk * g.EPW + s0) * N * D);
-          } else {  // env s0 + k's destination, from its agent-0 lane (NULL: masked)
-            const uint64_t pe = (uint64_t)(uintptr_t)my_obs;
-            const int src = (s0 + k) << g.lshift;
-            const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)pe, src);
-            const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(pe >> 32), src);
-            gdst = (unsigned char*)(uintptr_t)(((uint64_t)hi << 32) | lo);
-            if (!gdst) continue;
-          }
-          const uint32_t mis = (uint32_t)(uintptr_t)gdst & 15u;
-          const unsigned char* img = lds + g.off_stage + k * SE + mis;
-          const int nbytes = (one_run ? ne : 1) * run_bytes;
-          const int head = mis ? min(16 - (int)mis, nbytes) : 0;  // a multiple of 4
-          const int body = (nbytes - head) & ~15;
-          if (lane64 < head / 4) ((uint32_t*)gdst)[lane64] = ((const uint32_t*)img)[lane64];
-          const uint4* s4 = (const uint4*)(img + head);  // 16-byte aligned: mis + head
-          uint4* g4 = (uint4*)(gdst + head);
-          const int n16 = body / 16;
-          // four LDS reads in flight per lane before their stores
-          for (int i = lane64; i < n16; i += 256) {
-            const bool b1 = i + 64 < n16, b2 = i + 128 < n16, b3 = i + 192 < n16;
-            const uint4 v0 = s4[i];
-            uint4 v1, v2, v3;
-            if (b1) v1 = s4[i + 64];
-            if (b2) v2 = s4[i + 128];
-            if (b3) v3 = s4[i + 192];
-            g4[i] = v0;
-            if (b1) g4[i + 64] = v1;
-            if (b2) g4[i + 128] = v2;
-            if (b3) g4[i + 192] = v3;
-          }
-          const int tail = nbytes - head - body;
-          if (lane64 < tail / 4)
-            ((uint32_t*)(gdst + head + body))[lane64] = ((const uint32_t*)(img + head + body))[lane64];
-        }
+        copy_runs(gi, G);
         wave_fence();  // the next group's rows reuse the images
       }
     }
@@ -1567,7 +1599,8 @@ int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
       case 9: fn = partial_kernel<9, 0, 0>; break;
       default: return perr(MAPFX_EINVAL, "obs_window must be one of 0, 1, 3, 5, 7, 9");
     }
-  hipLaunchKernelGGL(fn, dim3(blocks), dim3(64), g.lds, (hipStream_t)stream, g, a);
+  const int nblk = (blocks + g.wpb - 1) / g.wpb;
+  hipLaunchKernelGGL(fn, dim3(nblk), dim3(64 * g.wpb), g.lds * g.wpb, (hipStream_t)stream, g, a);
   return check_hip(hipGetLastError(), "partial_kernel launch");
 }
 
@@ -1648,8 +1681,9 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.map_stride = mapfx_map_stride(c.H, c.W);
   g.map_env_bytes = round_up(g.rows * g.pitch, 16);
   g.bits_env_bytes = round_up(g.bits_words * 4 + 4, 16);
-  g.feat_env_bytes = round_up(64 * FR * 4, 16);
-  g.rew_env_bytes = 64 * 8;
+  g.feat_env_bytes = round_up(L * FR * 4, 16);  // (L lanes per env)
+  g.pos_env_bytes = round_up(L * 8, 16);
+  g.rew_env_bytes = round_up(L * 8, 16);
   g.gd32 = (long long)c.H * c.W > 32767 ? 1 : 0;  // a path is shorter than H * W cells
   g.big = (g.N > 64 || c.H > 256 || c.W > 256) ? 1 : 0;
   g.hs_log = 8;
@@ -1662,7 +1696,7 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.nc_rew = c.node_collide_reward;
   g.ec_rew = c.edge_collide_reward;
   g.env_rew = c.env_collide_reward;
-  const int per_env = 2 * g.map_env_bytes + g.bits_env_bytes + g.feat_env_bytes + 64 * 8 +
+  const int per_env = 2 * g.map_env_bytes + g.bits_env_bytes + g.feat_env_bytes + g.pos_env_bytes +
                       g.rew_env_bytes;
   // envs per wave: as many as fit 64 KB of LDS; one env may take up to the CU's
   // 160 KB (maps up to 256 x 256), with the dynamic-LDS limit raised below (the
@@ -1703,7 +1737,7 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.off_dep = off; off += EPW * g.map_env_bytes;
   g.off_bits = off; off += EPW * g.bits_env_bytes;
   g.off_feat = off; off += EPW * g.feat_env_bytes;
-  g.off_pos = off; off += EPW * 64 * 8;
+  g.off_pos = off; off += EPW * g.pos_env_bytes;
   g.off_rew = off; off += EPW * g.rew_env_bytes;
   // the fast observation path's staging images (one env's rows + 16 bytes of alignment
   // slack each) for a group of 64 lanes (the whole wave) or 32 (each half in turn),
@@ -1724,7 +1758,17 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
       }
     }
   }
-  g.lds = off;
+  g.lds = round_up(off, 16);
+  // waves per block: up to PARTIAL_MAX_WPB while the block's LDS fits the CU
+  g.wpb = 1;
+  if (!g.big) {
+    g.wpb = PARTIAL_MAX_WPB;
+    if (const char* ev = getenv("MAPFX_PARTIAL_WPB")) {  // diagnostic / A-B
+      const int v = atoi(ev);
+      if (v >= 1 && v <= PARTIAL_MAX_WPB) g.wpb = v;
+    }
+    while (g.wpb > 1 && g.wpb * g.lds > 160 * 1024) --g.wpb;
+  }
   if (g.big) {
     int rc0 = MAPFX_OK;
     if (g.wg_lds > 64 * 1024)
@@ -1746,13 +1790,14 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
       delete h;
       return rc0;
     }
-  } else if (g.lds > 64 * 1024) {
+  } else if (g.lds * g.wpb > 64 * 1024) {
     int rc0 = MAPFX_OK;
     for (auto fn : {partial_kernel<5, 5, 16>, partial_kernel<5, 5, 8>, partial_kernel<5, 5, 32>,
                     partial_kernel<3, 5, 16>, partial_kernel<7, 5, 16>, partial_kernel<0, 0, 0>,
                     partial_kernel<1, 0, 0>, partial_kernel<3, 0, 0>, partial_kernel<5, 0, 0>,
                     partial_kernel<7, 0, 0>, partial_kernel<9, 0, 0>})
-      if (!rc0) rc0 = check_hip(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, g.lds),
+      if (!rc0) rc0 = check_hip(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    g.lds * g.wpb),
                                 "hipFuncSetAttribute(partial_kernel LDS)");
     if (rc0) {
       delete h;

@@ -2162,7 +2162,10 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
 #ifndef MAPFX_PRIO_STORE
 #define MAPFX_PRIO_STORE 0
 #endif
-template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false, bool OCC = false>
+// ABT: the action block (0: MAPFX_AB); the split kernel has an 8-step instance for short
+// launches (T <= MAPFX_AB_SHORT_T): C2 T = 20 21.1 vs 21.9 us, while at T = 64 the 16-step
+// block stays faster (52.7 vs 57.0 us; tools/gpucmd_r04q.sh)
+template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false, bool OCC = false, int ABT = 0>
 // (split: 4 blocks per CU must be resident -- one wave per SIMD of each role -- so the
 // register budget is that of MAPFX_SPLIT_WAVES waves per SIMD)
 __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? MAPFX_SPLIT_WAVES : 1)
@@ -2282,7 +2285,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
 #ifndef MAPFX_AB
 #define MAPFX_AB 16
 #endif
-  constexpr int AB = ROLL ? MAPFX_AB : 1;
+  constexpr int AB = ROLL ? (ABT > 0 ? ABT : MAPFX_AB) : 1;
   uint32_t actpk[(AB + 3) / 4];
   // Action blocks from memory are prefetched one block ahead: block 0 is issued
   // with the state loads (its HBM latency overlaps the map build), block b + 1 as
@@ -3120,18 +3123,25 @@ int check_hip(hipError_t e, const char* what) {
 }
 
 
+#ifndef MAPFX_AB_SHORT_T
+#define MAPFX_AB_SHORT_T 32
+#endif
 template <int WIN>
-KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split, bool occ) {
+KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split, bool occ, bool short_t) {
   if (occ) {  // obs_window_occ: only the store-wave split writes it on the wave path
     if constexpr (WIN > 0 && (MAPFX_SPLIT_ALT || MAPFX_SPLIT_WAVES == 2)) {
-      if (roll && runner && split && fullw && L == 16) return mapf_wave_kernel<WIN, true, true, true, 16, true, true>;
+      if (roll && runner && split && fullw && L == 16)
+        return short_t ? mapf_wave_kernel<WIN, true, true, true, 16, true, true, 8>
+                       : mapf_wave_kernel<WIN, true, true, true, 16, true, true>;
     }
     return nullptr;
   }
   if (roll) {
     if (runner) {
       if constexpr (WIN > 0) {
-        if (split && fullw && L == 16) return mapf_wave_kernel<WIN, true, true, true, 16, true>;
+        if (split && fullw && L == 16)
+          return short_t ? mapf_wave_kernel<WIN, true, true, true, 16, true, false, 8>
+                         : mapf_wave_kernel<WIN, true, true, true, 16, true>;
       }
       if (!fullw) return mapf_wave_kernel<WIN, true, false, true, 0>;
       if (L == 16) return mapf_wave_kernel<WIN, true, true, true, 16>;
@@ -3144,12 +3154,12 @@ KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split, bo
   return fullw ? mapf_wave_kernel<WIN, false, true, false, 0> : mapf_wave_kernel<WIN, false, false, false, 0>;
 }
 
-KernelFn pick_wave_kernel(int win, bool roll, bool fullw, bool runner, int L, bool split, bool occ) {
+KernelFn pick_wave_kernel(int win, bool roll, bool fullw, bool runner, int L, bool split, bool occ, bool short_t) {
   switch (win) {
-    case 0: return pick_wave_win<0>(roll, fullw, runner, L, split, occ);
-    case 3: return pick_wave_win<3>(roll, fullw, runner, L, split, occ);
-    case 5: return pick_wave_win<5>(roll, fullw, runner, L, split, occ);
-    case 7: return pick_wave_win<7>(roll, fullw, runner, L, split, occ);
+    case 0: return pick_wave_win<0>(roll, fullw, runner, L, split, occ, short_t);
+    case 3: return pick_wave_win<3>(roll, fullw, runner, L, split, occ, short_t);
+    case 5: return pick_wave_win<5>(roll, fullw, runner, L, split, occ, short_t);
+    case 7: return pick_wave_win<7>(roll, fullw, runner, L, split, occ, short_t);
   }
   return nullptr;
 }
@@ -3181,7 +3191,8 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
                   (MAPFX_SPLIT_ALT ? SPLIT_FOLD_LDS : 0) + (MAPFX_SPLIT_MOVE ? SPLIT_RING_LDS : 0);
     const bool split = MAPFX_SPLIT && runner && fullw && g.L == 16 && g.wv_split_buf > 0 &&
                        split_lds <= 64 * 1024 && (al16 & 15) == 0;
-    KernelFn fn = pick_wave_kernel((a.obs_window || occ) ? g.window : 0, roll, fullw, runner, g.L, split, occ);
+    KernelFn fn = pick_wave_kernel((a.obs_window || occ) ? g.window : 0, roll, fullw, runner, g.L, split, occ,
+                                   roll && a.T <= MAPFX_AB_SHORT_T);
     if (fn) {
       const int blocks = (g.E + g.EPW - 1) / g.EPW;
       const dim3 bt(split ? 64 * MAPFX_SPLIT_WAVES : 64);

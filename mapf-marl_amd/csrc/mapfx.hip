@@ -2260,25 +2260,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
 
   const uint32_t oa = (uint32_t)(env * N + ag);  // agent index inside one step slot
   const uint32_t EN = (uint32_t)(g.E * N);
-  // bitmap words of this lane's first map rows (fast build): issued first
-  const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared || !env_ok ? 0 : (long long)env * g.map_stride));
-  // (the split kernel's three waves build the rows together: lane ag + 16 w of 48)
-  constexpr int RPF = SPLIT ? 1 : 4;
-  const int bl = SPLIT ? ag + LL * (int)(threadIdx.x >> 6) : ag, bnl = SPLIT ? LL * MAPFX_SPLIT_WAVES : L;
-  uint32_t pfw[RPF][3];
-  if (g.wv_fast) fast_row_prefetch<RPF>(g, bsrc, bl, bnl, pfw);
-  int tcur = env_ok ? a.t[env] : 0;  // (issued first: its pointer is preloaded)
-  int cur = 0, gcell = -1, st = 0;  // padded cell of the agent / of its goal
-  bool dn = false;
-  if (has) {
-    const int2 p = ((const int2*)a.pos)[oa];
-    const int2 q = ((const int2*)a.goal)[oa];
-    dn = a.done[oa] != 0;
-    cur = cell0 + p.x * pitch + p.y;
-    gcell = cell0 + q.x * pitch + q.y;
-    if (a.steps) st = a.steps[oa];
-  }
-  PSTAMP(0);
   const int T = ROLL ? a.T : 1;
   // Actions are fetched for AB steps at a time: one VMEM wait per block instead of
   // one per step (a wait on a per-step load would also drain the step's stores).
@@ -2288,7 +2269,8 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
   constexpr int AB = ROLL ? (ABT > 0 ? ABT : MAPFX_AB) : 1;
   uint32_t actpk[(AB + 3) / 4];
   // Action blocks from memory are prefetched one block ahead: block 0 is issued
-  // with the state loads (its HBM latency overlaps the map build), block b + 1 as
+  // first of all (its HBM latency overlaps the state loads and the map build; issued
+  // after them, step 0 still waited ~900 cycles for it at C2 T = 20), block b + 1 as
   // soon as block b is unpacked, so the wait at a block boundary finds it arrived.
   int nxt[AB];
   const bool act_mem = do_step && !a.use_rng;
@@ -2308,7 +2290,29 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
       for (int k = 0; k < AB; ++k) nxt[k] = (ap + (uint32_t)min(sb + k, T - 1) * EN)[oc_];
     }
   };
-  if (act_mem) fetch(0);
+  if (act_mem && ROLL) fetch(0);  // (one step: after the state loads -- a non-int8 action is
+                                  // range-checked at its load, which would wait for it here)
+
+  // bitmap words of this lane's first map rows (fast build): issued next
+  const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared || !env_ok ? 0 : (long long)env * g.map_stride));
+  // (the split kernel's three waves build the rows together: lane ag + 16 w of 48)
+  constexpr int RPF = SPLIT ? 1 : 4;
+  const int bl = SPLIT ? ag + LL * (int)(threadIdx.x >> 6) : ag, bnl = SPLIT ? LL * MAPFX_SPLIT_WAVES : L;
+  uint32_t pfw[RPF][3];
+  if (g.wv_fast) fast_row_prefetch<RPF>(g, bsrc, bl, bnl, pfw);
+  int tcur = env_ok ? a.t[env] : 0;  // (issued first: its pointer is preloaded)
+  int cur = 0, gcell = -1, st = 0;  // padded cell of the agent / of its goal
+  bool dn = false;
+  if (has) {
+    const int2 p = ((const int2*)a.pos)[oa];
+    const int2 q = ((const int2*)a.goal)[oa];
+    dn = a.done[oa] != 0;
+    cur = cell0 + p.x * pitch + p.y;
+    gcell = cell0 + q.x * pitch + q.y;
+    if (a.steps) st = a.steps[oa];
+  }
+  if (act_mem && !ROLL) fetch(0);
+  PSTAMP(0);
 
   // ---- padded map (from the bitmap: global -> registers, or staged in LDS), agents ----
   if (env_ok && !g.wv_fast) {

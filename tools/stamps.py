@@ -25,7 +25,7 @@ def main():
     b = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
                             episode_limit=2 ** 31 - 1, obs=("window",), window=5, track_steps=False)
     b.reset()
-    T = 64
+    T = int(os.environ.get("MAPFX_PROBE_T", 64))
     acts = b.gen_actions(T * 3, seed=2)
     traj = b._alloc_out(T)
     outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done", "traj_t")
@@ -35,7 +35,13 @@ def main():
     buf = (ctypes.c_ulonglong * (256 * 8))()
     mapfx.lib.mapfx_debug_stamps.restype = ctypes.c_int
     assert mapfx.lib.mapfx_debug_stamps(buf) == 0
-    st = np.array(buf, dtype=np.int64).reshape(256, 8)[:T]
+    full = np.array(buf, dtype=np.int64).reshape(256, 8)
+    st = full[:T]
+    pro = full[255]  # prologue: 6 entry, 0 state loads issued, 1 bitmap, 2 map built, 3 agents + neighbours
+    if pro[6] and pro[3]:
+        seq = [pro[6], pro[0], pro[1], pro[2], pro[3], st[0, 0]]
+        print("prologue (block 0 / lane 0, cycles): state loads issued %d, bitmap %d, map built %d, "
+              "agents + neighbours %d, -> step 0 %d" % tuple(np.diff(seq)))
     order = [0, 2, 1, 3, 4, 6]
     names = ["A move+atomics", "B rows+fold", "C heavy+tail", "D nbrs+dones", "end barrier/fence"]
     print("E=%d  s_memtime cycles per step segment (median / mean over steps 1..T-2)" % E)

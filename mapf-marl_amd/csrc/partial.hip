@@ -37,6 +37,12 @@
 #include "mapfx.h"
 #include "mapfx_partial.h"
 
+#ifndef PARTIAL_STAGE_FIRST
+// 1: partial_kernel stages the bitmap before issuing the state loads (its wait then covers
+// one load, not all; the map build overlaps the rest).  Measured round 4: 15.73 vs
+// 15.42 us per step (gpurun_out/r04u) -- slower, so off.
+#define PARTIAL_STAGE_FIRST 0
+#endif
 #ifndef PABL
 #define PABL 0  // diagnostic builds only: 1 skip the obs rows, 2 skip the step, 4 skip the staged copy
 #endif
@@ -946,6 +952,15 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   const bool nb_carry = a.pnbr && a.pdist && !g.gd32;  // neighbour distances carried
   const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)ec_ * g.map_stride));
   const uint32_t bw0 = bsrc[ag < g.bits_words ? ag : 0];  // this lane's first bitmap word
+#if PARTIAL_STAGE_FIRST
+  // the bitmap staged before the state loads are issued: the wait is for this one load
+  // (after the state loads the compiler's wait covered all of them), and the map build
+  // then overlaps their latency
+  if (env_ok) {
+    if (ag < g.bits_words) bitsL[ag] = bw0;
+    for (int w = ag + g.L; w < g.bits_words; w += g.L) bitsL[w] = bsrc[w];  // maps past 16 x 32 words
+  }
+#endif
   // the step's action: one 8-byte load of the aligned block that holds it (whatever the
   // dtype: the block lies in the element's page), decoded after the map build; the
   // runner's address needs the env's row of the MAC output first
@@ -981,10 +996,12 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
     epl_raw = a.ra.ep_length[ec_];
   }
   // ---- LDS map (c format) + dep map (obstacle flag in bit 7) ----
+#if !PARTIAL_STAGE_FIRST
   if (env_ok) {
     if (ag < g.bits_words) bitsL[ag] = bw0;
     for (int w = ag + g.L; w < g.bits_words; w += g.L) bitsL[w] = bsrc[w];  // maps past 16 x 32 words
   }
+#endif
   PST(1);
   wave_fence();
   if (env_ok) {

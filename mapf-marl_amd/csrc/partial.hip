@@ -37,6 +37,9 @@
 #include "mapfx.h"
 #include "mapfx_partial.h"
 
+#ifndef PARTIAL_EARLY_WB
+#define PARTIAL_EARLY_WB 1  // partial_kernel: state / avail / post rows stored right after the step
+#endif
 #ifndef PARTIAL_STAGE_FIRST
 // 1: partial_kernel stages the bitmap before issuing the state loads (its wait then covers
 // one load, not all; the map build overlaps the rest).  Measured round 4: 15.73 vs
@@ -1223,6 +1226,80 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   const int nbd2 = gt[c > 0 ? -1 : 0], nbd3 = gt[c + 1 < g.W ? 1 : 0];
 
   PST(8);
+#if PARTIAL_EARLY_WB
+  // ---- the step's results leave before the observation rows are built: their stores
+  // then queue ahead of the rows' copy-out instead of behind it ----
+  // avail (:399-433): neighbour in bounds and not a free-standing obstacle
+  uint32_t am = 16u;
+  if (has && (a.avail || a.ra.ep_avail)) {
+    if (map[cur - pitch]) am |= 1u;
+    if (map[cur + pitch]) am |= 2u;
+    if (map[cur - 1]) am |= 4u;
+    if (map[cur + 1]) am |= 8u;
+    if (a.avail) a.avail[oa] = (uint8_t)am;
+  }
+  // state (:377-387): [total collisions, step count, sum(each goal cost)]
+  const int gsum = group_sum(has ? gcost : 0, g.L);
+  if (env_ok && ag == 0 && a.state) {
+    a.state[3 * env + 0] = (float)total;
+    a.state[3 * env + 1] = (float)tcur;
+    a.state[3 * env + 2] = (float)gsum;
+  }
+  // ---- state write-back ----
+  if (has) {
+    ((int2*)a.pos)[oa] = make_int2(r, c);
+    a.steps[oa] = steps;
+    a.at_goal[oa] = at_goal ? 1 : 0;
+    a.done[oa] = dn ? 1 : 0;
+    a.goal_cost[oa] = gcost;
+    a.node[oa] = (uint8_t)node;
+    a.edge[oa] = edge;
+    if (a.pdist) a.pdist[oa] = pd;
+    if (runner && arow >= 0) {  // the EpisodeBatch's actions / actions_onehot rows at ts
+      const long long v = act_value(alo, ahi);
+      if (a.ra.ep_actions)
+        a.ra.ep_actions[(long long)env * a.ra.ep_actions_sb + (long long)a.ra.ts * a.ra.ep_actions_st + ag] = v;
+      if (a.ra.ep_onehot) {
+        float* oh = a.ra.ep_onehot + (long long)env * a.ra.ep_onehot_sb +
+                    (long long)a.ra.ts * a.ra.ep_onehot_st + (long long)ag * 5;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) oh[k] = v == k ? 1.0f : 0.0f;
+      }
+    }
+  }
+  if (env_ok && ag == 0) {
+    a.t[env] = tcur;
+    a.terminated[env] = term ? 1 : 0;
+    a.total_coll[env] = total;
+  }
+  if (post && env_ok) {  // runner_post_kernel (runner.hip) for a running env, fused
+    const mapfx_runner_acts& ra = a.ra;
+    if (live0) {
+      if (ag == 0) {
+        if (ra.ep_reward) ra.ep_reward[(long long)env * ra.ep_reward_sb + (long long)ra.ts * ra.ep_reward_st] = (float)Rsum;
+        // env_terminated = terminated and not info.get("episode_limit") (parallel_runner.py:146-150):
+        // MARL_PARTIAL's info has no "episode_limit" key
+        if (ra.ep_term) ra.ep_term[(long long)env * ra.ep_term_sb + (long long)ra.ts * ra.ep_term_st] = term ? 1 : 0;
+        ra.ep_return[env] = epr0 + Rsum;
+        ra.ep_length[env] = epl0 + 1;
+        ra.alive[env] = term ? 0 : 1;
+        if (ra.ep_state) {  // update(pre_transition_data, bs, ts + 1): state, avail, filled
+          float* d = ra.ep_state + (long long)env * ra.ep_state_sb;
+          d[0] = (float)total;
+          d[1] = (float)tcur;
+          d[2] = (float)gsum;
+        }
+        if (ra.ep_filled) ra.ep_filled[(long long)env * ra.ep_filled_sb] = 1;
+      }
+      if (has && ra.ep_avail) {
+        int32_t* d = ra.ep_avail + (long long)env * ra.ep_avail_sb + ag * 5;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) d[k] = (int32_t)((am >> k) & 1u);
+      }
+    }
+    if (ag == 0) ra.alive_prev[env] = live0;
+  }
+#endif
   // ---- observations of the current state (:312-391) ----
   // per-agent feature rows: curr, start, goal, unit vec, norm, node, edge, steps
   if (has) {
@@ -1447,6 +1524,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   }
   PST(11);
   (void)o;
+#if !PARTIAL_EARLY_WB
   // avail (:399-433): neighbour in bounds and not a free-standing obstacle
   uint32_t am = 16u;
   if (has && (a.avail || a.ra.ep_avail)) {
@@ -1473,7 +1551,6 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
     a.node[oa] = (uint8_t)node;
     a.edge[oa] = edge;
     if (a.pdist) a.pdist[oa] = pd;
-    if (nb_carry) ((uint2*)a.pnbr)[oa] = nb1;
     if (runner && arow >= 0) {  // the EpisodeBatch's actions / actions_onehot rows at ts
       const long long v = act_value(alo, ahi);
       if (a.ra.ep_actions)
@@ -1518,6 +1595,9 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
     }
     if (ag == 0) ra.alive_prev[env] = live0;
   }
+#endif
+  // the carried neighbour distances are stored last (their loads land during the rows)
+  if (has && nb_carry) ((uint2*)a.pnbr)[oa] = nb1;
   PST(12);
 #ifdef PARTIAL_STAMPS
   __builtin_amdgcn_s_waitcnt(0);

@@ -64,13 +64,14 @@ def parse():
                     help="target CPU work of the cpu_baseline sample (0 disables)")
     ap.add_argument("--no-gather", action="store_true",
                     help="N > 1: skip the RCCL gather leg (reported beside the compute-only value)")
-    ap.add_argument("--gather-payload", default="occ",
+    ap.add_argument("--gather-payload", default="compact",
                     choices=("occ", "planes", "reward_done", "compact"),
-                    help="what each chunk gathers to rank 0: occ = obs_window_occ (the window as "
-                         "one occupancy plane, half the bytes of the two planes) + reward + done; "
-                         "planes = obs_window + reward + done; reward_done = reward + done only "
-                         "(observations consumed on-rank); compact = reward + u16 cell + done bit "
-                         "per agent-step (rank 0 rebuilds observations with mapfx_observe)")
+                    help="what each chunk gathers to rank 0: compact (default) = reward + u16 "
+                         "cell + done bit per agent-step (rank 0 rebuilds observations with "
+                         "mapfx_observe; the payload whose rank-0 ingress keeps up with the compute "
+                         "at 8 ranks); occ = obs_window_occ (the window as one occupancy plane) + "
+                         "reward + done; planes = obs_window + reward + done; reward_done = reward "
+                         "+ done only (observations consumed on-rank)")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="CPU/gloo rehearsal of the multi-rank launch + shard + packed gather")
     ap.add_argument("--selftest-envs", type=int, default=6)
@@ -297,6 +298,8 @@ def main():
         pl()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    from mapfx import _abi
+    kernel_name = _abi.last_kernel()    # the instance the timed launches ran
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -346,6 +349,7 @@ def main():
                 b2.step(acts[k % na], outputs=pouts)
         graph.replay()
         torch.cuda.synchronize()
+        step_kernel = _abi.last_kernel()
         pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 3
         t1 = time.perf_counter()
@@ -364,14 +368,15 @@ def main():
         cb = canonical_bytes_per_env_step(S, S, N, W)
         # HBM bytes per launch of the per-step kernel from its own PMC profile
         # (profiles/pmc_<config>_step.json, taken of this bench command)
-        ptraffic, ptraffic_src = profile_traffic("%s_step" % args.config, config=args.config + "_step",
-                                                 T=1, E=E)
+        ptraffic, ptraffic_src = profile_traffic("%s_step" % args.config, kernel=step_kernel,
+                                                 config=args.config + "_step", T=1, E=E)
         per_step = {
             "value": round(E * N * reps * ks / pel * world, 1),
             "ms_per_step": round(pel / (reps * ks) * 1e3, 5),
             "kernel_ms": round(pk_ms, 5),
             "eager_ms_per_step": round(eager_ms, 5),
             "launch": "HIP graph of %d mapfx_step launches, replayed" % ks,
+            "kernel": step_kernel,
             "roofline": {"bound": "hbm", "achieved": round(E * cb / (pk_ms * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(E * cb / (pk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -403,19 +408,8 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(inst, S, N, E, W, args.cpu_seconds)
 
-    traffic, traffic_src = None, None
-    pmc_path = args.pmc or os.path.join(REPO, "profiles", "pmc_%s.json" % args.config)
-    try:
-        with open(pmc_path) as f:
-            pm = json.load(f)
-        if pm.get("config") == args.config and pm.get("T") == T and pm.get("E") == E \
-                and pm.get("traffic_bytes_per_launch"):
-            traffic = pm["traffic_bytes_per_launch"]
-            traffic_src = "%s: %s" % (os.path.relpath(pmc_path, REPO),
-                                      pm.get("command", "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
-                                                        "passes at T=%d" % T))
-    except (OSError, ValueError):
-        pass
+    traffic, traffic_src = profile_traffic(args.config, kernel=kernel_name, path=args.pmc,
+                                           config=args.config, T=T, E=E)
 
     if rank == 0:
         line = {
@@ -446,6 +440,8 @@ def main():
                           else "")},
             "env_steps_per_s": round(total_envs * K / elapsed, 1),
             "kernel_ms_per_launch": round(kern_ms, 5),
+            "kernel": kernel_name,
+            "build_id": _abi.build_id(),
             "timing": {"wall_ms": round(elapsed * 1e3, 4),
                        "kernel_ms_events": round(kern_ms_total, 4),
                        "kernel_timing": "per-launch start/stop events recorded at the "
@@ -510,6 +506,7 @@ def time_gather(dist, b, acts, outs, T, k0, K, world, E, N, keys, payload):
     per_chunk = int(og.bytes_per_chunk())
     ingress = (world - 1) * per_chunk
     return {"value": round(world * E * N * nch * T / el, 1),
+            "ingress_arithmetic": payload_arithmetic(T, E, N, b.window, world),
             "ms_per_step": round(el / (nch * T) * 1e3, 5),
             "steps": nch * T, "chunk_steps": T, "payload": payload, "keys": list(keys),
             "bytes_per_rank_per_chunk": per_chunk,
@@ -520,27 +517,63 @@ def time_gather(dist, b, acts, outs, T, k0, K, world, E, N, keys, payload):
                           "stream, packed %s buffer" % "+".join(keys)}
 
 
+def payload_arithmetic(T, E, N, W, world):
+    """Bytes per rank per T-step chunk of each --gather-payload (16-B aligned fields, as
+    mapfx.dist.ChunkLayout lays them out) and rank 0's xGMI ingress time at N ranks:
+    (world - 1) chunks over (world - 1) links of XGMI_LINK_GBS each."""
+    al = lambda n: -(-n // 16) * 16   # noqa: E731
+    fields = {"compact": (8 * T * E, 2 * T * E * N, T * E * ((N + 7) // 8)),
+              "occ": (T * E * N * W * W, 8 * T * E, T * E * N),
+              "planes": (2 * T * E * N * W * W, 8 * T * E, T * E * N),
+              "reward_done": (8 * T * E, T * E * N)}
+    out = {}
+    for k, f in fields.items():
+        per = sum(al(x) for x in f)
+        out[k] = {"bytes_per_rank_per_chunk": per,
+                  "rank0_ingress_bytes_per_chunk": (world - 1) * per,
+                  "ingress_bound_ms_per_chunk": round(per / (XGMI_LINK_GBS * 1e9) * 1e3, 5)
+                  if world > 1 else 0.0}
+    return out
+
+
 PARTIAL_YAML = dict(  # MARL-curve-main/src/config/envs/marl_partial.yaml:3-23
     obs_window=5, obs_knn_agents=5, episode_limit=100, move_reward=0, stay_reward=-0.1,
     stay_goal_reward=1, node_collide_reward=-2000, edge_collide_reward=-2000,
     env_collide_reward=-2000, complete_reward=1000, complete_fac=1.5, gamma=0.99)
 
 
-def profile_traffic(leg, **match):
-    """(traffic bytes per unit, source) from profiles/pmc_<leg>.json when every `match`
-    key equals the profile's (the profile was taken of this exact workload), else
-    (None, None).  The file is written by tools/pmc_traffic.py from separate
-    rocprofv3 FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md corrections)."""
-    path = os.path.join(REPO, "profiles", "pmc_%s.json" % leg)
+def kernel_instance(name):
+    """The instance part of a demangled kernel name (tools/pmc_traffic.instance)."""
+    i = name.find("<")
+    j = name.find("(", i) if i >= 0 else -1
+    return (name[:j] if j > 0 else name).strip()
+
+
+def profile_traffic(leg, kernel=None, path=None, **match):
+    """(traffic bytes per launch, source) from profiles/pmc_<leg>.json, or (None, why).
+    The file is written by tools/pmc_traffic.py from separate rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes (MI355X_MICROARCH.md corrections).  It is cited only when it was
+    taken of THIS build (its build_id equals mapfx_build_id of the loaded library), of
+    the same kernel instance the bench just launched (`kernel`, mapfx_last_kernel) and
+    of this workload (every `match` key equal); otherwise traffic is null and the
+    reason is reported instead of a stale figure."""
+    from mapfx import _abi
+    path = path or os.path.join(REPO, "profiles", "pmc_%s.json" % leg)
+    rel = os.path.relpath(path, REPO)
     try:
         with open(path) as f:
             pm = json.load(f)
     except (OSError, ValueError):
-        return None, None
-    if any(pm.get(k) != v for k, v in match.items()) or not pm.get("traffic_bytes_per_launch"):
-        return None, None
-    return pm["traffic_bytes_per_launch"], "%s: %s" % (os.path.relpath(path, REPO),
-                                                       pm.get("command", "rocprofv3 --pmc passes"))
+        return None, "no profile %s" % rel
+    if pm.get("build_id") != _abi.build_id():
+        return None, "refused %s: taken of build %r, running %r" % (rel, pm.get("build_id"),
+                                                                    _abi.build_id())
+    if kernel is not None and kernel_instance(pm.get("kernel", "")) != kernel_instance(kernel):
+        return None, "refused %s: profiled kernel %r, launched %r" % (rel, pm.get("kernel"), kernel)
+    bad = [k for k, v in match.items() if pm.get(k) != v]
+    if bad or not pm.get("traffic_bytes_per_launch"):
+        return None, "refused %s: workload keys %s differ" % (rel, bad)
+    return pm["traffic_bytes_per_launch"], "%s: %s" % (rel, pm.get("command", "rocprofv3 --pmc passes"))
 
 
 def partial_bytes_per_env_step(N, D, HW):
@@ -626,11 +659,13 @@ def run_partial(args, dist, rank, world, local):
         b.step(acts[k])
     torch.cuda.synchronize()
     eager_ms = (time.perf_counter() - t1) / limit * 1e3
+    from mapfx import _abi
+    kernel_name = _abi.last_kernel()     # the step instance the graph replays
     D = b.obs_dim
     bpes = partial_bytes_per_env_step(N, D, S * S)
     achieved = E * bpes / (kern_ms * 1e-3) / 1e9
     # traffic per launch (one env step of E envs) from the PMC profile of this workload
-    traffic, traffic_src = profile_traffic("partial", E=E, N=N, S=S)
+    traffic, traffic_src = profile_traffic("partial", kernel=kernel_name, E=E, N=N, S=S)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = partial_cpu_baseline(inst, S, N, args.cpu_seconds)
@@ -650,6 +685,7 @@ def run_partial(args, dist, rank, world, local):
             "env_steps_per_s": round(E * world * K / elapsed, 1),
             "kernel_ms_per_step": round(kern_ms, 5),
             "eager_ms_per_step": round(eager_ms, 5),
+            "kernel": kernel_name, "build_id": _abi.build_id(),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
@@ -713,6 +749,8 @@ def run_primal(args, dist, rank, world, local):
     for pr in ev:
         b.act(ids, acts, events=pr)
     torch.cuda.synchronize()
+    from mapfx import _abi
+    kernel_name = _abi.last_kernel()
     kern_list = sorted(a0.elapsed_time(a1) for a0, a1 in ev)
     kern_ms = kern_list[len(kern_list) // 2]
     el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -726,7 +764,7 @@ def run_primal(args, dist, rank, world, local):
     achieved = launch_bytes / (kern_ms * 1e-3) / 1e9
     # the profile is keyed by what tools/pmc_traffic.py records: config, calls per launch
     # (T) and worlds (E); the bench's fixed 32 x 32 / 16 agents / s = 10 shape is implied
-    traffic, traffic_src = profile_traffic("primal", config="primal", E=E, T=KC)
+    traffic, traffic_src = profile_traffic("primal", kernel=kernel_name, config="primal", E=E, T=KC)
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         from oracle.primal_dyn_oracle import PrimalWorld
@@ -758,6 +796,7 @@ def run_primal(args, dist, rank, world, local):
                                    % (E, N, s_obs, KC, R),
                        "envs_total": E * world, "agents": N, "parallelism": "env-shard x%d" % world},
             "kernel_ms_per_launch": round(kern_ms, 5),
+            "kernel": kernel_name, "build_id": _abi.build_id(),
             "timing": {"kernel_ms_launches": [round(x, 5) for x in kern_list],
                        "stream_ms_per_launch": round(wall_kern_ms, 5),
                        "kernel_timing": "per-launch start/stop events recorded at the kernel's "

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MAPFX_ABI_VERSION 4
+#define MAPFX_ABI_VERSION 5
 
 /* error codes */
 #define MAPFX_OK 0
@@ -128,6 +128,18 @@ typedef struct mapfx_info {
 
 int mapfx_abi_version(void);
 const char* mapfx_last_error(void);
+
+/* Identity of this build (ABI 5): "src=<first 16 hex of the sha256 over the HIP
+ * sources, headers and compile flags> git=<commit the build started from>[+dirty]",
+ * fixed at compile time.  A profile records it, so a measurement can refuse a profile
+ * taken of another build (bench.py, tools/pmc_traffic.py). */
+const char* mapfx_build_id(void);
+/* Demangled name of the env kernel the calling thread launched last through this
+ * library (the MAPF step / rollout / observe, the MARL_PARTIAL step / reset / observe,
+ * the PRIMAL act; not the helper kernels: BFS tables, masked resets, action generation,
+ * packing, runner bookkeeping), exactly as rocprofv3 names it; "" before the first
+ * launch.  Needs the HIP runtime (a visible device).  ABI 5. */
+const char* mapfx_last_kernel(void);
 
 /* Bytes of one env's obstacle bitmap: ceil(H*W/8) rounded up to 16. */
 int64_t mapfx_map_stride(int32_t H, int32_t W);

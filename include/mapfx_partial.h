@@ -111,7 +111,10 @@ int32_t mapfx_partial_obs_dim(const mapfx_partial_t* h);
 int32_t mapfx_partial_goal_dist_elem_size(int32_t H, int32_t W);
 
 /* BFS distance tables of every (masked) env's goals (:906-928: A* lengths on
- * the 4-connected free-cell graph == BFS levels). */
+ * the 4-connected free-cell graph == BFS levels).  The carried distances of the
+ * recomputed envs become stale with their tables, so st->pdist (when non-NULL) is
+ * set to INT32_MIN for them: their next step looks the distances up again, as the
+ * reference reads _goal_dist afresh every step (:228-229). */
 int mapfx_partial_goal_dist(mapfx_partial_t* h, const mapfx_partial_state* st,
                             const uint8_t* env_mask, void* stream);
 

@@ -9,6 +9,8 @@ extern "C" {
 #endif
 // sets the message returned by mapfx_last_error(); returns `code`
 int mapfx_internal_error(int code, const char* msg);
+// records the host stub of the kernel the calling thread just launched (mapfx_last_kernel)
+void mapfx_note_kernel(const void* fn);
 // partial.hip: mapfx_partial_step with the observation rows written to an EpisodeBatch
 // time row (obs_rows + e * obs_env_stride floats, only envs with obs_mask[e] != 0)
 int mapfx_partial_step_rows(mapfx_partial_t* h, const mapfx_partial_state* st, const void* actions,

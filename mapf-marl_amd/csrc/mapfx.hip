@@ -26,8 +26,10 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <cxxabi.h>
 #include <math.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -43,6 +45,9 @@
 namespace {
 
 thread_local std::string g_last_error;
+
+// the host stub of the calling thread's most recent launch (mapfx_last_kernel)
+thread_local const void* g_last_kernel = nullptr;
 
 int set_error(int code, const char* fmt, ...) {
   char buf[512];
@@ -3205,6 +3210,7 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
         hipExtLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, ev0, ev1, 0, MAPFX_HOT_ARGS(a, g, blocks), a, g);
       else
         hipLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, MAPFX_HOT_ARGS(a, g, blocks), a, g);
+      g_last_kernel = (const void*)fn;
       return check_hip(hipGetLastError(), "mapf_wave_kernel launch");
     }
   }
@@ -3216,6 +3222,7 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
     hipExtLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, ev0, ev1, 0, MAPFX_HOT_ARGS(a, g, blocks), a, g);
   else
     hipLaunchKernelGGL(fn, dim3(blocks), dim3(g.BT), lds, stream, MAPFX_HOT_ARGS(a, g, blocks), a, g);
+  g_last_kernel = (const void*)fn;
   return check_hip(hipGetLastError(), roll ? "mapf_rollout_kernel launch" : "mapf_step_kernel launch");
 }
 
@@ -3274,6 +3281,31 @@ int check_out(const mapfx_t* h, const mapfx_out* o) {
 extern "C" {
 
 int mapfx_abi_version(void) { return MAPFX_ABI_VERSION; }
+
+#ifndef MAPFX_BUILD_ID
+#define MAPFX_BUILD_ID "src=unknown git=unknown"
+#endif
+const char* mapfx_build_id(void) { return MAPFX_BUILD_ID; }
+
+void mapfx_note_kernel(const void* fn) { g_last_kernel = fn; }
+
+const char* mapfx_last_kernel(void) {
+  thread_local std::string name;
+  thread_local const void* named = nullptr;
+  if (!g_last_kernel) return "";
+  if (named != g_last_kernel) {
+    const char* raw = hipKernelNameRefByPtr(g_last_kernel, nullptr);
+    name = raw ? raw : "";
+    if (raw && raw[0] == '_' && raw[1] == 'Z') {
+      int status = 0;
+      char* dem = abi::__cxa_demangle(raw, nullptr, nullptr, &status);
+      if (status == 0 && dem) name = dem;
+      free(dem);
+    }
+    named = g_last_kernel;
+  }
+  return name.c_str();
+}
 
 // error hook for the other translation unit of the library (partial.hip)
 int mapfx_internal_error(int code, const char* msg) { return set_error(code, "%s", msg); }

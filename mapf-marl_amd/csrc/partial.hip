@@ -1608,6 +1608,18 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
+// A goal-table rebuild makes the carried distances stale: pdist of every (masked) env
+// becomes PD_NONE, so its next step looks the current and target cells up in the new
+// table (marl_partial.py:228-229 reads _goal_dist afresh every step); pnbr is only read
+// while pdist is valid
+__global__ void __launch_bounds__(256) pdist_invalidate_kernel(long long total, int N, const uint8_t* env_mask,
+                                                               int32_t* pdist) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  if (env_mask && !env_mask[i / N]) return;
+  pdist[i] = PD_NONE;
+}
+
 // sqrt(i), i = 0 .. n, with the same device sqrt isqrt_f64 uses (mapfx_partial_create
 // compares it bit for bit with host libm before the kernels may use it)
 __global__ void __launch_bounds__(256) sqrt_probe_kernel(double* out, int n) {
@@ -1622,7 +1634,7 @@ struct mapfx_partial_t {
   PGeo geo;
   double* bonus_lut;
   int device;
-  int no_nbcarry;  // diagnostic / A-B (MAPFX_PARTIAL_NBCARRY=0): ignore the state's pnbr
+  int no_nbcarry;  // diagnostic builds (MAPFX_PARTIAL_DIAG_ENV) only: ignore the state's pnbr
 };
 
 namespace {
@@ -1678,6 +1690,7 @@ int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
     void (*fn)(PGeo, PArgs) = pick_wg(g.win, wg_apl(g));
     if (!fn) return perr(MAPFX_EINVAL, "obs_window must be one of 0, 1, 3, 5, 7, 9");
     hipLaunchKernelGGL(fn, dim3(g.E), dim3(WG_THREADS), g.wg_lds, (hipStream_t)stream, g, a);
+    mapfx_note_kernel((const void*)fn);
     return check_hip(hipGetLastError(), "partial_wg_kernel launch");
   }
   const int blocks = (g.E + g.EPW - 1) / g.EPW;
@@ -1698,6 +1711,7 @@ int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
     }
   const int nblk = (blocks + g.wpb - 1) / g.wpb;
   hipLaunchKernelGGL(fn, dim3(nblk), dim3(64 * g.wpb), g.lds * g.wpb, (hipStream_t)stream, g, a);
+  mapfx_note_kernel((const void*)fn);
   return check_hip(hipGetLastError(), "partial_kernel launch");
 }
 
@@ -1750,7 +1764,9 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   h->cfg = c;
   h->bonus_lut = nullptr;
   h->no_nbcarry = 0;
+#ifdef MAPFX_PARTIAL_DIAG_ENV  // A/B knobs read from the environment: diagnostic builds only
   if (const char* ev = getenv("MAPFX_PARTIAL_NBCARRY")) h->no_nbcarry = atoi(ev) == 0;
+#endif
   if (hipGetDevice(&h->device) != hipSuccess) h->device = 0;
   PGeo& g = h->geo;
   memset(&g, 0, sizeof(g));
@@ -1800,10 +1816,12 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   // workgroup path keeps no map in LDS)
   int EPW = g.big ? 1 : 64 / L;
   while (EPW > 1 && EPW * per_env > 64 * 1024) --EPW;
+#ifdef MAPFX_PARTIAL_DIAG_ENV
   if (const char* ev = getenv("MAPFX_PARTIAL_EPW")) {  // diagnostic / A-B: fewer envs per wave
     const int v = atoi(ev);
     if (v >= 1 && v < EPW) EPW = v;
   }
+#endif
   if (!g.big && EPW * per_env > 160 * 1024) {
     delete h;
     return perr(MAPFX_EINVAL, "one env needs more than 160 KB of LDS (map too large)");
@@ -1860,10 +1878,12 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.wpb = 1;
   if (!g.big) {
     g.wpb = PARTIAL_MAX_WPB;
+#ifdef MAPFX_PARTIAL_DIAG_ENV
     if (const char* ev = getenv("MAPFX_PARTIAL_WPB")) {  // diagnostic / A-B
       const int v = atoi(ev);
       if (v >= 1 && v <= PARTIAL_MAX_WPB) g.wpb = v;
     }
+#endif
     while (g.wpb > 1 && g.wpb * g.lds > 160 * 1024) --g.wpb;
   }
   if (g.big) {
@@ -1996,7 +2016,12 @@ int mapfx_partial_goal_dist(mapfx_partial_t* h, const mapfx_partial_state* st,
       hipLaunchKernelGGL(partial_bfs_big_kernel<int16_t>, grid, dim3(256), 0, sm, g, st->map_bits,
                          st->goal, env_mask, (int16_t*)st->goal_dist);
   }
-  return check_hip(hipGetLastError(), "partial_bfs_kernel launch");
+  rc = check_hip(hipGetLastError(), "partial_bfs_kernel launch");
+  if (rc || !st->pdist) return rc;
+  const long long total = (long long)g.E * g.N;
+  hipLaunchKernelGGL(pdist_invalidate_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, sm, total,
+                     g.N, env_mask, st->pdist);
+  return check_hip(hipGetLastError(), "pdist_invalidate_kernel launch");
 }
 
 int mapfx_partial_reset(mapfx_partial_t* h, const mapfx_partial_state* st, const uint8_t* env_mask,

@@ -931,6 +931,7 @@ int mapfx_primal_act_timed(mapfx_primal_t* h, const mapfx_primal_state* st, cons
                             (hipEvent_t)start_event, (hipEvent_t)stop_event, 0, g, a);
     else
       hipLaunchKernelGGL(pick_seq(g), dim3(g.E), dim3(64), g.lds_seq, (hipStream_t)stream, g, a);
+    mapfx_note_kernel((const void*)pick_seq(g));
     return check_hip(hipGetLastError(), "primal_seq_kernel launch");
   }
   const int wpw = 64 >> g.lw_shift;
@@ -939,6 +940,7 @@ int mapfx_primal_act_timed(mapfx_primal_t* h, const mapfx_primal_state* st, cons
                           (hipEvent_t)start_event, (hipEvent_t)stop_event, 0, g, a);
   else
     hipLaunchKernelGGL(pick_primal(g), dim3((g.E + wpw - 1) / wpw), dim3(64), h->lds, (hipStream_t)stream, g, a);
+  mapfx_note_kernel((const void*)pick_primal(g));
   return check_hip(hipGetLastError(), "primal_act_kernel launch");
 }
 

@@ -86,7 +86,8 @@ class QOut(ctypes.Structure):
 
 # every symbol include/mapfx.h, include/mapfx_partial.h and include/mapfx_primal.h declare
 # (checked by tests/test_abi_exports.py)
-EXPORTS = ("mapfx_abi_version", "mapfx_last_error", "mapfx_map_stride", "mapfx_obs_elem_size",
+EXPORTS = ("mapfx_abi_version", "mapfx_last_error", "mapfx_build_id", "mapfx_last_kernel",
+           "mapfx_map_stride", "mapfx_obs_elem_size",
            "mapfx_edge_elem_size",
            "mapfx_create", "mapfx_destroy", "mapfx_query", "mapfx_reset", "mapfx_step",
            "mapfx_observe", "mapfx_rollout", "mapfx_rollout_timed", "mapfx_gen_actions", "mapfx_action",
@@ -111,7 +112,7 @@ class RState(ctypes.Structure):  # include/mapfx_runner.h mapfx_runner_state
                             "env_steps", "env_actions", "bs_inv")]
 
 
-ABI_VERSION = 4  # include/mapfx.h MAPFX_ABI_VERSION
+ABI_VERSION = 5  # include/mapfx.h MAPFX_ABI_VERSION
 
 
 class MapfxError(RuntimeError):
@@ -127,6 +128,8 @@ def _load():
     sig = {
         "mapfx_abi_version": (c_i32, []),
         "mapfx_last_error": (ctypes.c_char_p, []),
+        "mapfx_build_id": (ctypes.c_char_p, []),
+        "mapfx_last_kernel": (ctypes.c_char_p, []),
         "mapfx_map_stride": (c_i64, [c_i32, c_i32]),
         "mapfx_obs_elem_size": (c_i32, [c_i32]),
         "mapfx_edge_elem_size": (c_i32, [c_i32]),
@@ -180,6 +183,16 @@ def check(rc: int, what: str):
     if rc != 0:
         msg = lib.mapfx_last_error()
         raise MapfxError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+
+def build_id() -> str:
+    """mapfx_build_id(): "src=<sources sha256[:16]> git=<head>[+dirty]" of the loaded library."""
+    return lib.mapfx_build_id().decode()
+
+
+def last_kernel() -> str:
+    """mapfx_last_kernel(): the rocprofv3 name of this thread's last env-kernel launch."""
+    return lib.mapfx_last_kernel().decode()
 
 
 def ptr(t) -> int | None:

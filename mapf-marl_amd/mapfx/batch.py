@@ -326,17 +326,20 @@ class MapfGridBatch:
         """Overwrite the device state (pos [E,N,2] int32 (row, col), optional done /
         t) -- e.g. positions unpacked from a compact gather, to rebuild their
         observations with observe().  Positions are checked to lie on the grid (one
-        host sync): the kernels index their LDS cell maps with them."""
-        p = torch.as_tensor(pos, device=self.device).view(self.E, self.N, 2)
+        host sync): the kernels index their LDS cell maps with them.  A position on
+        an obstacle cell is legal state (quirk 1: agents may stand on obstacles, e.g.
+        transposed .scen starts) and is observed exactly as the reference would.
+        Any strided input (a slice of unpack_compact's output) is accepted."""
+        p = torch.as_tensor(pos, device=self.device).to(torch.int32).reshape(self.E, self.N, 2)
         lo = torch.tensor([0, 0], device=self.device)
         hi = torch.tensor([self.H, self.W], device=self.device)
         if p.numel() and not bool(((p >= lo) & (p < hi)).all()):
             raise ValueError("positions outside the %dx%d grid" % (self.H, self.W))
         self.pos.copy_(p)
         if done is not None:
-            self.done.copy_(torch.as_tensor(done, device=self.device).view(self.E, self.N))
+            self.done.copy_(torch.as_tensor(done, device=self.device).reshape(self.E, self.N))
         if t is not None:
-            self.t.copy_(torch.as_tensor(t, device=self.device).view(self.E))
+            self.t.copy_(torch.as_tensor(t, device=self.device).reshape(self.E))
 
     def host_mirror(self):
         """Pinned host copy of the packed buffer and its typed views (packed=True)."""

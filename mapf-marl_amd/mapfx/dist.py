@@ -126,9 +126,24 @@ def compact_spec(T, E, N):
             "done_bits": ((T, E, (N + 7) // 8), torch.uint8)}
 
 
-def pack_compact_host(traj_pos, traj_done, W, cell, done_bits):
+COMPACT_MAX_CELLS = 65536   # cells travel as u16 row * W + col
+
+
+def check_compact_grid(H, W):
+    """The compact payload's u16 cell index needs H * W <= 65536 (mapfx_pack_compact
+    refuses larger grids; a host-side cast would wrap silently)."""
+    if int(H) * int(W) > COMPACT_MAX_CELLS:
+        raise ValueError("compact gather payload: cells are u16, H * W = %d > %d"
+                         % (int(H) * int(W), COMPACT_MAX_CELLS))
+
+
+def pack_compact_host(traj_pos, traj_done, W, cell, done_bits, H=None):
     """mapfx_pack_compact for CPU tensors (the gloo tests' oracle stand-in batch;
     device batches use the HIP kernel)."""
+    if H is not None:
+        check_compact_grid(H, W)
+    if traj_pos.numel() and int(traj_pos[..., 0].max()) * int(W) + int(W) > COMPACT_MAX_CELLS:
+        raise ValueError("compact gather payload: a cell index exceeds u16 (W = %d)" % int(W))
     c = traj_pos[..., 0] * int(W) + traj_pos[..., 1]
     cell.copy_(c.to(torch.int32).to(torch.int16))
     N = traj_done.shape[-1]
@@ -166,6 +181,12 @@ class OverlappedGather:
     compact=True gathers COMPACT_KEYS instead of `keys`: the reward row plus every
     agent-step's u16 cell and done bit, packed by mapfx_pack_compact on the side
     stream (about a tenth of the occupancy-window payload).
+
+    Uneven shards (mapfx.dist.shard of an env count the world does not divide): the
+    ranks exchange their env counts once at construction; every rank sends the
+    largest rank's prefix size (its own prefix, then padding), so the collective's
+    equal-size contract holds, and result(i) returns one dict of views per rank, each
+    cut to that rank's env count, instead of [world, ...] views.
     """
 
     def __init__(self, batch, T: int, keys=("obs_window", "reward", "traj_done"), outputs=None,
@@ -177,6 +198,7 @@ class OverlappedGather:
         self.compact = bool(compact)
         spec = dict(batch.out_spec(self.T))
         if self.compact:   # the gathered prefix is COMPACT_KEYS, packed from the rollout
+            check_compact_grid(batch.H, batch.W)
             keys = COMPACT_KEYS
             spec.update(compact_spec(self.T, batch.E, batch.N))
             if outputs is not None:
@@ -186,14 +208,25 @@ class OverlappedGather:
         self.outputs = outputs
         self.dst, self.group = dst, group
         self.layout = ChunkLayout(spec, order=self.keys)
-        # whole 16-B units, so every typed view of a received row stays aligned
-        self.gbytes = -(-self.layout.end_of(self.keys) // ChunkLayout.ALIGN) * ChunkLayout.ALIGN
         dev = batch.device
         self.cuda = torch.device(dev).type == "cuda"
-        self.flat = [self.layout.alloc(dev), self.layout.alloc(dev)]
-        self.bufs = [self.layout.views(f) for f in self.flat]
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        # every rank's env count (one small all-reduce at construction)
+        counts = torch.zeros(self.world, dtype=torch.int64, device=dev)
+        counts[self.rank] = int(batch.E)
+        dist.all_reduce(counts, group=group)
+        self.rank_envs = [int(c) for c in counts.tolist()]
+        self.even = len(set(self.rank_envs)) == 1
+        # each rank's gathered prefix (its own layout: the env dimension of every
+        # gathered [T, E, ...] tensor is that rank's count), whole 16-B units so every
+        # typed view of a received row stays aligned
+        self.rank_layouts = [self._layout_for(spec, e) for e in self.rank_envs]
+        self.gbytes = max(-(-lay.end_of(self.keys) // ChunkLayout.ALIGN) * ChunkLayout.ALIGN
+                          for lay in self.rank_layouts)
+        nb = max(self.layout.nbytes, self.gbytes)
+        self.flat = [torch.zeros(nb, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.bufs = [self.layout.views(f) for f in self.flat]
         self.recv = None
         if self.rank == dst:
             self.recv = [torch.empty((self.world, self.gbytes), dtype=torch.uint8, device=dev)
@@ -220,7 +253,7 @@ class OverlappedGather:
             if self.compact:
                 b = self.bufs[cur]
                 pack_compact_host(b["traj_pos"], b["traj_done"], self.batch.W, b["cell"],
-                                  b["done_bits"])
+                                  b["done_bits"], H=self.batch.H)
             self._gather(cur)
             self.i += 1
             return i
@@ -248,16 +281,28 @@ class OverlappedGather:
         self._check(i)
         return self.bufs[i & 1]
 
+    def _layout_for(self, spec, envs):
+        """The gathered keys' layout for a rank holding `envs` envs: every gathered
+        tensor is [T, E, ...], so only its env dimension changes."""
+        sub = {}
+        for k in self.keys:
+            shape, dt = spec[k]
+            sub[k] = ((shape[0], int(envs)) + tuple(shape[2:]), dt)
+        return ChunkLayout(sub, order=self.keys)
+
     def result(self, i):
         """On dst: chunk i's gathered tensors, key -> [world, T, E_rank, ...] (rank
-        order = global env order).  Valid until step_chunk(i + 2) is called."""
+        order = global env order); with uneven shards a list over ranks of
+        key -> [T, E_r, ...].  Valid until step_chunk(i + 2) is called."""
         self._check(i)
         if self.rank != self.dst:
             return None
         cur = i & 1
         if self.cuda and self.gather_ev[cur] is not None:
             torch.cuda.current_stream(self.batch.device).wait_event(self.gather_ev[cur])
-        return self.layout.views(self.recv[cur], self.keys)
+        if self.even:
+            return self.layout.views(self.recv[cur], self.keys)
+        return [lay.views(self.recv[cur][r], self.keys) for r, lay in enumerate(self.rank_layouts)]
 
     def _check(self, i):
         if not self.i - 2 <= i < self.i:

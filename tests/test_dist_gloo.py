@@ -177,7 +177,7 @@ class _OracleTrajBatch:
         from oracle import corc
         self.corc = corc
         self.E, self.N, self.win, self.offset = inst["init_pos"].shape[0], N, W, offset
-        self.W = S   # grid width (MapfGridBatch.W), what the compact payload's cells use
+        self.H = self.W = S   # grid size (MapfGridBatch.H / W), what the compact cells use
         self.device = torch.device("cpu")
         self.ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=7,
                                    env_offset=offset, nthreads=1)
@@ -277,3 +277,83 @@ def test_overlapped_gather_packed_world2(keys):
             # [world, T, E_rank, ...] -> [T, world * E_rank, ...]
             merged = np.concatenate(list(g[k]), axis=1)
             assert np.array_equal(merged.view(np.uint8), traj[k].numpy().view(np.uint8)), (i, k)
+
+
+def _og_uneven_worker(rank, world, port, q, n_total, compact):
+    import sys
+    sys.path[:0] = [REPO, PKG_ROOT]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mapfx.dist import OverlappedGather, shard
+        from mapfx.maps import synthetic_instances
+        c = _OG
+        off, cnt = shard(n_total, rank, world)
+        inst = synthetic_instances(cnt, c["S"], c["S"], c["N"], p_obstacle=0.1, seed=5, env_offset=off)
+        fb = _OracleTrajBatch(inst, c["S"], c["N"], c["W"], off)
+        keys = "compact" if compact else ("obs_window_occ", "reward", "traj_done")
+        og = OverlappedGather(fb, c["T"], keys=keys, compact=compact)
+        assert not og.even and og.rank_envs == [shard(n_total, r, world)[1] for r in range(world)]
+        got = []
+        for i in range(c["chunks"]):
+            og.step_chunk(seed=9, t0=i * c["T"])
+            res = og.result(i)
+            if rank == 0:
+                got.append([{k: v.clone().numpy() for k, v in part.items()} for part in res])
+        if rank == 0:
+            q.put(got)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_overlapped_gather_uneven_world3(compact):
+    """World 3 over gloo with uneven shards (mapfx.dist.shard of 8 envs: 3 / 3 / 2):
+    every rank sends the largest rank's prefix size, rank 0 gets one view dict per
+    rank cut to that rank's env count, and the concatenation equals an unsharded run."""
+    from mapfx.maps import synthetic_instances
+    world, c, n_total = 3, _OG, 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_og_uneven_worker, args=(r, world, port, q, n_total, compact))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    inst = synthetic_instances(n_total, c["S"], c["S"], c["N"], p_obstacle=0.1, seed=5)
+    fb = _OracleTrajBatch(inst, c["S"], c["N"], c["W"], 0)
+    for i in range(c["chunks"]):
+        traj = {k: torch.zeros(s, dtype=d) for k, (s, d) in fb.out_spec(c["T"]).items()}
+        fb.rollout(c["T"], seed=9, t0=i * c["T"], traj=traj)
+        parts = got[i]
+        assert [p_["reward"].shape[1] for p_ in parts] == [3, 3, 2]
+        if compact:
+            from mapfx.dist import unpack_compact
+            us = [unpack_compact({k: torch.from_numpy(v) for k, v in p_.items()}, c["S"], c["N"])
+                  for p_ in parts]
+            for k, ref in (("reward", "reward"), ("pos", "traj_pos"), ("done", "traj_done")):
+                merged = np.concatenate([u[k].numpy() for u in us], axis=1)
+                assert np.array_equal(merged.view(np.uint8), traj[ref].numpy().view(np.uint8)), (i, k)
+            continue
+        for k in ("obs_window_occ", "reward", "traj_done"):
+            merged = np.concatenate([p_[k] for p_ in parts], axis=1)
+            assert np.array_equal(merged.view(np.uint8), traj[k].numpy().view(np.uint8)), (i, k)
+
+
+def test_compact_refuses_large_grid():
+    """The compact payload's cells are u16: a grid above 65536 cells is refused before
+    anything is packed (the host pack would otherwise wrap silently)."""
+    from mapfx.dist import check_compact_grid, pack_compact_host
+    check_compact_grid(256, 256)
+    with pytest.raises(ValueError):
+        check_compact_grid(257, 256)
+    pos = torch.zeros((1, 1, 1, 2), dtype=torch.int32)
+    with pytest.raises(ValueError):
+        pack_compact_host(pos, torch.zeros((1, 1, 1), dtype=torch.uint8), 300,
+                          torch.zeros((1, 1, 1), dtype=torch.int16),
+                          torch.zeros((1, 1, 1), dtype=torch.uint8), H=300)

@@ -16,7 +16,7 @@ from conftest import PKG_ROOT, REPO
 
 pytestmark = pytest.mark.gpu
 
-C = dict(S=32, N=16, E=64, T=5, chunks=3, W=5, seed=17)
+C = dict(S=32, N=16, T=5, chunks=3, W=5, seed=17)
 KEYS = ("obs_window_occ", "reward", "traj_done")
 
 
@@ -38,7 +38,7 @@ def _batch(mapfx, E, offset):
     return b
 
 
-def _worker(rank, world, port, q, compact):
+def _worker(rank, world, port, q, compact, n_total):
     import sys
     sys.path[:0] = [REPO, PKG_ROOT]
     import torch.distributed as dist
@@ -48,8 +48,9 @@ def _worker(rank, world, port, q, compact):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import mapfx
-        from mapfx.dist import OverlappedGather
-        b = _batch(mapfx, C["E"], rank * C["E"])
+        from mapfx.dist import OverlappedGather, shard
+        off, cnt = shard(n_total, rank, world)
+        b = _batch(mapfx, cnt, off)
         outs = ("reward", "term", "node", "edge", "avail", "obs_window_occ", "traj_pos", "traj_done",
                 "traj_t")
         og = OverlappedGather(b, C["T"], keys=KEYS, outputs=outs, compact=compact)
@@ -58,7 +59,10 @@ def _worker(rank, world, port, q, compact):
             og.step_chunk(seed=C["seed"], t0=i * C["T"])
             res = og.result(i)
             if rank == 0:
-                got.append({k: v.cpu().numpy().copy() for k, v in res.items()})
+                parts = res        # uneven shards: one dict per rank already
+                if og.even:        # [world, T, E, ...] -> one dict per rank
+                    parts = [{k: v[r] for k, v in res.items()} for r in range(world)]
+                got.append([{k: v.cpu().numpy().copy() for k, v in p_.items()} for p_ in parts])
         og.synchronize()
         if rank == 0:
             q.put(got)
@@ -66,39 +70,43 @@ def _worker(rank, world, port, q, compact):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("compact", [False, True])
-def test_two_rank_shards_gather_equals_unsharded(compact):
+@pytest.mark.parametrize("world,n_total,compact", [(2, 128, False), (2, 128, True),
+                                                   (3, 160, True), (3, 160, False)])
+def test_two_rank_shards_gather_equals_unsharded(world, n_total, compact):
     """compact=True: the gathered payload is the reward row + u16 cells + done bits
     (mapfx_pack_compact on the side stream); unpacked it equals the unsharded
     trajectory, and rank 0 rebuilds every step's window from the unpacked positions
-    with mapfx_observe, bit for bit the window the rollout wrote."""
+    with mapfx_observe, bit for bit the window the rollout wrote.  World 3 shards
+    160 envs unevenly (54 / 53 / 53, mapfx.dist.shard): every rank sends the largest
+    prefix, rank 0 cuts each rank's part to its env count."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     import mapfx
     import torch.multiprocessing as mp
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, compact)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, compact, n_total))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=100)
     for p in procs:
         p.join(timeout=30)
         assert p.exitcode == 0
-    full = _batch(mapfx, world * C["E"], 0)
-    obs_b = _batch(mapfx, world * C["E"], 0)      # rank 0's observation rebuilder
+    full = _batch(mapfx, n_total, 0)
+    obs_b = _batch(mapfx, n_total, 0)      # rank 0's observation rebuilder
     for i in range(C["chunks"]):
         traj = full.rollout(C["T"], seed=C["seed"], t0=i * C["T"])
         if compact:
             from mapfx.dist import COMPACT_KEYS, unpack_compact
-            assert tuple(got[i]) == COMPACT_KEYS
-            u = unpack_compact({k: torch.from_numpy(v) for k, v in got[i].items()}, C["S"], C["N"])
+            assert all(tuple(p_) == COMPACT_KEYS for p_ in got[i])
+            us = [unpack_compact({k: torch.from_numpy(v) for k, v in p_.items()}, C["S"], C["N"])
+                  for p_ in got[i]]
             for k, ref in (("reward", "reward"), ("pos", "traj_pos"), ("done", "traj_done")):
-                merged = np.concatenate(list(u[k].numpy()), axis=1)
+                merged = np.concatenate([u[k].numpy() for u in us], axis=1)
                 assert np.array_equal(merged.view(np.uint8), traj[ref].cpu().numpy().view(np.uint8)), (i, k)
-            pos = torch.cat(list(u["pos"]), dim=1)                   # [T, world * E, N, 2]
+            pos = torch.cat([u["pos"] for u in us], dim=1)            # [T, n_total, N, 2]
             for k in range(C["T"]):
                 obs_b.set_positions(pos[k])
                 o = obs_b.observe()
@@ -106,6 +114,6 @@ def test_two_rank_shards_gather_equals_unsharded(compact):
                 assert torch.equal(o["obs_window_occ"], traj["obs_window_occ"][k]), (i, k)
             continue
         for k in KEYS:
-            merged = np.concatenate(list(got[i][k]), axis=1)      # [world, T, E, ...] -> [T, 2E, ...]
+            merged = np.concatenate([p_[k] for p_ in got[i]], axis=1)   # -> [T, n_total, ...]
             ref = traj[k].cpu().numpy()
             assert np.array_equal(merged.view(np.uint8), ref.view(np.uint8)), (i, k)

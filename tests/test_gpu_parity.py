@@ -267,6 +267,7 @@ def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T, obs, win):
 
 @pytest.mark.parametrize("E,T,win,autoreset,N", [
     (4096, 64, 5, False, 16),   # the bench shape
+    (4096, 20, 5, False, 16),   # the driver's shape: T <= 32 takes the 8-step action-block instance
     (256, 1, 5, False, 16), (256, 2, 5, False, 16), (256, 3, 3, False, 16), (252, 17, 7, False, 16),
     (64, 40, 5, True, 16),
     (250, 12, 5, False, 12), (130, 9, 3, True, 7), (66, 10, 5, False, 40),  # N < L
@@ -352,6 +353,100 @@ def test_runner_rollout_agents_on_obstacles(mapfx_mod, autoreset):
             b2.reset(env_mask=out["term"].clone())
     assert np.array_equal(_np(b1.pos), _np(b2.pos))
     assert np.array_equal(_np(b1.t), _np(b2.t))
+
+
+# the instance pick_wave_win chooses for the bench's C2 launch (mapfx.hip): T <= 32 takes
+# the 8-step action block, longer launches the default 16-step one (template arg 0)
+C2_SPLIT_INSTANCE = {20: "mapf_wave_kernel<5, true, true, true, 16, true, false, 8>",
+                     64: "mapf_wave_kernel<5, true, true, true, 16, true, false, 0>"}
+
+
+@pytest.mark.parametrize("T", [20, 64, 33])
+def test_bench_rollout_matches_oracle_every_step(mapfx_mod, T):
+    """The driver's exact launch (bench.py --steps 20: C2, 4096 envs, int8 actions resident
+    in HBM, the bench's output set, one launch of T = 20) against the C oracle at EVERY
+    step: reward bits, node, edge, avail, term, window, positions, dones and t.  The
+    launch must be the instance the bench times (checked by name); T = 64 is the default
+    bench chunk, T = 33 the first launch past the short-block threshold."""
+    from mapfx import _abi
+    from mapfx.maps import synthetic_instances
+    from oracle import corc
+    import bench
+    S, N, E, p, _ = bench.CONFIGS["c2"]
+    inst = synthetic_instances(E, S, S, N, p_obstacle=p, seed=1)
+    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                                episode_limit=2 ** 31 - 1, obs=("window",), window=5,
+                                track_steps=False)
+    ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=2 ** 31 - 1)
+    b.reset()
+    acts = b.gen_actions(T, seed=2)
+    traj = b._alloc_out(T)
+    traj.pop("reward_f32")
+    outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done", "traj_t")
+    b.rollout_plan(T, actions=acts, traj=traj, outputs=outs, stream=torch.cuda.current_stream())()
+    name = _abi.last_kernel()
+    if T in C2_SPLIT_INSTANCE:
+        assert C2_SPLIT_INSTANCE[T] in name, name
+    torch.cuda.synchronize()
+    ah = _np(acts).astype(np.int32)
+    for k in range(T):
+        r = ob.step(ah[k])
+        o = ob.observe(window=5, full=False)
+        assert np.array_equal(_u64(_np(traj["reward"][k])), _u64(r["reward"])), k
+        assert np.array_equal(_np(traj["node"][k]), r["node"]), k
+        assert np.array_equal(_np(traj["edge"][k]), r["edge"]), k
+        assert np.array_equal(_np(traj["avail"][k]), o["avail"]), k
+        assert np.array_equal(_np(traj["term"][k]), o["term"]), k
+        assert np.array_equal(_np(traj["obs_window"][k]), o["obs_window"]), k
+        assert np.array_equal(_np(traj["traj_pos"][k]), ob.pos), k
+        assert np.array_equal(_np(traj["traj_done"][k]), ob.done), k
+        assert np.array_equal(_np(traj["traj_t"][k]), ob.t), k
+    assert np.array_equal(_np(b.pos), ob.pos) and np.array_equal(_np(b.t), ob.t)
+
+
+def test_back_to_back_rollout_launches(mapfx_mod):
+    """Launches that read the state the previous launch wrote back, enqueued back to back
+    with no host wait between them (the bench's timed region: C3, 2048 envs of 64
+    agents on the shared warehouse map, 8 launches), equal the oracle's one long
+    rollout: every launch's last step and the final state.  A launch overlapping its
+    predecessor (VERDICT r04 weak #8) would read stale positions here."""
+    from mapfx import _abi
+    from oracle import corc
+    import bench
+    S, N, E, _, shared = bench.CONFIGS["c3"]
+    inst = _instances(mapfx_mod, E, S, N, None, shared, seed=1)
+    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                                episode_limit=2 ** 31 - 1, obs=("window",), window=5,
+                                track_steps=False)
+    ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=2 ** 31 - 1)
+    b.reset()
+    T, L = 16, 8
+    acts = b.gen_actions(T * L, seed=2)
+    outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done", "traj_t")
+    trajs = []
+    for i in range(L):
+        tr = b._alloc_out(T)
+        tr.pop("reward_f32")
+        trajs.append(tr)
+    plans = [b.rollout_plan(T, actions=acts[i * T:(i + 1) * T], traj=trajs[i], outputs=outs,
+                            stream=torch.cuda.current_stream()) for i in range(L)]
+    torch.cuda.synchronize()
+    for pl in plans:
+        pl()
+    assert "mapf_wave_kernel<5, true, true, true, 64" in _abi.last_kernel(), _abi.last_kernel()
+    torch.cuda.synchronize()
+    ah = _np(acts).astype(np.int32)
+    for i in range(L):
+        for k in range(T):
+            r = ob.step(ah[i * T + k])
+        o = ob.observe(window=5, full=False)
+        tr = trajs[i]
+        assert np.array_equal(_u64(_np(tr["reward"][-1])), _u64(r["reward"])), i
+        assert np.array_equal(_np(tr["edge"][-1]), r["edge"]), i
+        assert np.array_equal(_np(tr["obs_window"][-1]), o["obs_window"]), i
+        assert np.array_equal(_np(tr["traj_pos"][-1]), ob.pos), i
+        assert np.array_equal(_np(tr["traj_t"][-1]), ob.t), i
+    assert np.array_equal(_np(b.pos), ob.pos) and np.array_equal(_np(b.done), ob.done)
 
 
 def test_rollout_matches_oracle_long_horizon(mapfx_mod):

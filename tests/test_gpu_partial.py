@@ -172,6 +172,124 @@ def test_partial_bench_shape_matches_oracle(mapfx_mod):
         assert np.array_equal(_np(out["avail"]), np.stack([_mask5(r.avail()) for r in refs])), t
 
 
+def _bench_actions(mapfx_mod, inst, S, N, T):
+    """bench.py --env marl_partial's actions: the device generator (seed 2) of a
+    MapfGridBatch over the same instances, [T, E, N] int8 in HBM."""
+    ga = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                                 obs=(), track_steps=False)
+    return ga.gen_actions(T, seed=2)
+
+
+def test_partial_bench_episode_matches_oracle(mapfx_mod):
+    """the bench's whole replayed episode at its shape (yaml config, empty
+    8x8, 15 agents, 4096 envs, the generator's int8 actions): reset + 100 steps (the
+    episode limit: every env terminates at t = 100) + a second reset + 5 steps, every
+    64th env and the last against the CPU restatement at every step.  Every other
+    sampled env has its goals on its starts and stays put at steps 0 and 40, so the
+    completion bonus (marl_partial.py:291-299) fires at 4096 envs; the second reset
+    re-initialises the carried goal distances (pdist / pnbr, ABI 4) that every step
+    after it uses."""
+    from mapfx.maps import synthetic_instances
+    from oracle.partial_oracle import PartialEnvState
+    import bench
+    S, N, E = 8, 15, 4096
+    limit = bench.PARTIAL_YAML["episode_limit"]
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.0, seed=1)
+    sample = list(range(5, E, 64)) + [E - 1]
+    complete = sample[::2]
+    goals = inst["goals"].copy()
+    goals[complete] = inst["init_pos"][complete]
+    grid = np.zeros((S, S), dtype=np.int8)
+    b = mapfx_mod.MarlPartialBatch(inst["init_pos"], goals, grids=grid[None], **bench.PARTIAL_YAML)
+    refs = {e: PartialEnvState(grid, inst["init_pos"][e], goals[e], **bench.PARTIAL_YAML) for e in sample}
+    acts = _bench_actions(mapfx_mod, inst, S, N, limit)
+    acts[0, complete] = 4
+    acts[40, complete] = 4
+    ah = _np(acts).astype(np.int64)
+    idx = torch.tensor(sample, device="cuda")
+    bonus_seen = 0
+
+    def check(out, t, rr=None):
+        nonlocal bonus_seen
+        obs = _np(out["obs"][idx])
+        for j, e in enumerate(sample):
+            r = refs[e]
+            assert np.array_equal(obs[j], r.obs().astype(np.float32)), (t, e)
+            assert np.array_equal(_np(out["avail"][e]), _mask5(r.avail())), (t, e)
+            assert np.array_equal(_np(out["state"][e]), r.state().astype(np.float32)), (t, e)
+            assert np.array_equal(_np(b.pos[e]), np.array(r.pos)), (t, e)
+            if rr is not None:
+                rew, term = rr[e]
+                got = _np(out["reward"][e:e + 1])
+                assert got.view(np.uint64)[0] == np.float64(rew).view(np.uint64), (t, e, got, rew)
+                assert bool(_np(b.terminated[e:e + 1])[0]) == bool(term), (t, e)
+                bonus_seen += int(rew > 100)
+
+    for ep in range(2):
+        out = b.reset()
+        for r in refs.values():
+            r.reset()
+        check(out, -1)
+        for t in range(limit if ep == 0 else 5):
+            out = b.step(acts[t])
+            rr = {e: refs[e].step(ah[t, e]) for e in sample}
+            check(out, t, rr)
+        if ep == 0:
+            assert _np(b.terminated).all() and (_np(b.t) == limit).all()   # the episode limit
+    assert bonus_seen >= len(complete)
+
+
+def test_partial_carried_distances_equal_lookup(mapfx_mod):
+    """the carried goal distances (pdist / pnbr, ABI 4) give the same episode
+    as the table lookups a binding without them gets (NULL pointers), and a step right
+    after set_agents() (new goals, new tables, no reset) uses the new tables: equal to
+    the lookup path and to the restatement with the new goals."""
+    from oracle.partial_oracle import PartialEnvState, bfs_goal_dist
+    from tests_helpers_partial import largest_component
+    rng = np.random.default_rng(11)
+    S, N, E, T = 12, 6, 24, 12
+    kw = dict(obs_window=5, obs_knn_agents=5, episode_limit=60, move_reward=-0.01,
+              stay_reward=-0.02, stay_goal_reward=0.5, node_collide_reward=-1.5,
+              edge_collide_reward=-2, env_collide_reward=-3, complete_reward=1000,
+              complete_fac=1.5, gamma=0.99)
+    grid = largest_component((rng.random((S, S)) < 0.15).astype(np.int8) * -1)
+    free = np.argwhere(grid == 0)
+    picks = [rng.choice(len(free), size=3 * N, replace=False) for _ in range(E)]
+    inits = np.array([free[p[:N]] for p in picks])
+    goals = np.array([free[p[N:2 * N]] for p in picks])
+    goals2 = np.array([free[p[2 * N:]] for p in picks])
+    carried = mapfx_mod.MarlPartialBatch(inits, goals, grids=grid[None], **kw)
+    lookup = mapfx_mod.MarlPartialBatch(inits, goals, grids=grid[None], **kw)
+    lookup._state.pdist = None
+    lookup._state.pnbr = None
+    assert carried.pnbr is not None          # int16 tables: the carried path is on
+    refs = [PartialEnvState(grid, inits[e], goals[e], **kw) for e in range(E)]
+    carried.reset()
+    lookup.reset()
+    acts = rng.integers(0, 5, size=(2 * T, E, N))
+    for t in range(2 * T):
+        if t == T:   # new goals mid-episode, tables rebuilt, no reset
+            mask = np.zeros(E, dtype=bool)
+            mask[::2] = True
+            g_new = np.where(mask[:, None, None], goals2, goals)
+            for bb in (carried, lookup):
+                bb.set_agents(inits, g_new, env_mask=mask)
+            for e in np.flatnonzero(mask):
+                refs[e].goals = [tuple(int(v) for v in p) for p in goals2[e]]
+                refs[e].goal_dist = [bfs_goal_dist(refs[e].grid, g) for g in refs[e].goals]
+                refs[e]._refresh()
+        a = torch.from_numpy(acts[t]).cuda()
+        oc = carried.step(a)
+        rc = _np(oc["reward"]).copy()
+        obs_c = _np(oc["obs"]).copy()
+        ol = lookup.step(a)
+        assert np.array_equal(rc.view(np.uint64), _np(ol["reward"]).view(np.uint64)), t
+        assert np.array_equal(obs_c, _np(ol["obs"])), t
+        ref = np.array([r.step(acts[t, e])[0] for e, r in enumerate(refs)], dtype=np.float64)
+        assert np.array_equal(rc.view(np.uint64), ref.view(np.uint64)), t
+        assert np.array_equal(obs_c, np.stack([r.obs() for r in refs]).astype(np.float32)), t
+
+
 def test_partial_dropin_output_mode(mapfx_mod, tmp_path):
     """MARL_PARTIAL_ENV(output=True) through the registry against the reference run
     with output=True (mp_out8_n5): the drop-in draws the same instance with the same

@@ -85,11 +85,17 @@ def _make_runner(tmp_path, fx, B, mac, **extra):
     return runner, logger
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("name", CASES)
-def test_runner_matches_reference_parallel_runner(tmp_path, name):
+def test_runner_matches_reference_parallel_runner(tmp_path, name, fused):
+    """fused=False: the runner state without bs_inv (a binding that predates ABI 4), so
+    mapfx_runner_step takes the separate actions / env step / post kernels instead of
+    the fused env step; both must fill the batch exactly as the reference runner."""
     from conftest import load_fixture
     fx = load_fixture(name)
     runner, logger = _make_runner(tmp_path, fx, int(fx["B"]), ScriptedMAC())
+    if not fused:
+        runner._rs.bs_inv = None
     for r in range(int(fx["runs"])):
         batch = runner.run(test_mode=False)
         for k, v in batch.data.transition_data.items():

@@ -3,6 +3,13 @@
 
   python tools/pmc_traffic.py --trace DIR --fetch DIR --write DIR [--lds DIR] --out profiles/pmc_c2.json
       [--kernel mapf_rollout_kernel] [--config c2 --T 64 --E 4096] [--command "..."]
+      [--bench-json DIR/bench_traced.json]
+
+* --bench-json: the bench line of the profiled command.  Its "kernel" (the exact
+  instance the bench launched, mapfx_last_kernel) selects the kernel in every pass
+  instead of the --kernel substring, and its "build_id" (mapfx_build_id: source
+  hash + git head) is recorded: bench.py cites the profile only for that same build
+  and kernel instance.
 
 * --trace: a `rocprofv3 --kernel-trace --stats --output-format csv` directory; the
   per-kernel stats CSV is copied and the kernel's average duration recorded.
@@ -39,10 +46,26 @@ def _col(row, *names):
     raise KeyError(names)
 
 
+def instance(name):
+    """The kernel instance part of a demangled name: up to the parameter list that
+    follows the template arguments (rocprofv3 and __cxa_demangle agree on it)."""
+    i = name.find("<")
+    j = name.find("(", i) if i >= 0 else -1
+    return (name[:j] if j > 0 else name).strip()
+
+
+def kernel_match(kernel, name):
+    """--kernel is a substring; a full demangled name (from --bench-json) must name the
+    same instance."""
+    if "<" in kernel:
+        return instance(kernel) == instance(name)
+    return kernel in name
+
+
 def pmc_values(d, kernel, counter):
     per_dispatch = {}
     for r in _rows(d, "*counter_collection.csv"):
-        if kernel not in _col(r, "Kernel_Name", "KernelName"):
+        if not kernel_match(kernel, _col(r, "Kernel_Name", "KernelName")):
             continue
         if _col(r, "Counter_Name", "CounterName") != counter:
             continue
@@ -66,21 +89,28 @@ def trace_stats(d, kernel, out_dir, tag):
         with open(p, newline="") as f:
             for r in csv.DictReader(f):
                 name = _col(r, "Name", "KERNEL_NAME", "Kernel_Name")
-                if kernel in name:
+                if kernel_match(kernel, name):
                     res.setdefault("kernels", []).append({
-                        "name": name[:160], "calls": int(float(_col(r, "Calls"))),
+                        "name": name, "calls": int(float(_col(r, "Calls"))),
                         "avg_ns": float(_col(r, "AverageNs", "Average_Ns")),
                         "total_ns": float(_col(r, "TotalDurationNs", "Total_Duration_Ns"))})
     # per-dispatch durations from the kernel trace
     durs = []
-    rows = [r for r in _rows(d, "*kernel_trace.csv") if kernel in _col(r, "Kernel_Name", "KernelName")]
+    rows = [r for r in _rows(d, "*kernel_trace.csv")
+            if kernel_match(kernel, _col(r, "Kernel_Name", "KernelName"))]
     rows.sort(key=lambda r: int(_col(r, "Start_Timestamp")))
+    starts, ends = [], []
     for r in rows:
-        durs.append(int(_col(r, "End_Timestamp")) - int(_col(r, "Start_Timestamp")))
+        s0, e0 = int(_col(r, "Start_Timestamp")), int(_col(r, "End_Timestamp"))
+        starts.append(s0)
+        ends.append(e0)
+        durs.append(e0 - s0)
     if durs:
         res["dispatches"] = len(durs)
         res["median_ns"] = statistics.median(durs)
         res["dispatch_ns"] = durs   # in launch order
+        # begin of dispatch i + 1 minus end of dispatch i (negative: the two overlapped)
+        res["gap_ns"] = [starts[i + 1] - ends[i] for i in range(len(starts) - 1)]
     return res
 
 
@@ -151,13 +181,29 @@ def main():
     ap.add_argument("--lds", default=None)
     ap.add_argument("--command", default=None)
     ap.add_argument("--sq", default=None, help="a `rocprofv3 --pmc` pass of SQ_COUNTERS")
+    ap.add_argument("--bench-json", default=None,
+                    help="bench line of the profiled command: exact kernel instance + build id")
+    ap.add_argument("--bench-kernel-key", default="kernel",
+                    help="dotted key of the kernel name in the bench line (per_step.kernel for the "
+                         "per-step leg)")
     ap.add_argument("--match", action="append", default=[],
                     help="key=int stored in the summary (bench.py only uses a profile whose "
                          "keys equal its workload's)")
     a = ap.parse_args()
     out_dir = os.path.dirname(os.path.abspath(a.out))
     os.makedirs(out_dir, exist_ok=True)
+    if a.bench_json:
+        with open(a.bench_json) as f:
+            line = json.loads([x for x in f.read().splitlines() if x.startswith("{")][-1])
+        kname = line
+        for part in a.bench_kernel_key.split("."):
+            kname = (kname or {}).get(part)
+        if not kname or not line.get("build_id"):
+            raise SystemExit("%s carries no %s / build_id" % (a.bench_json, a.bench_kernel_key))
+        a.kernel = kname
     res = {"config": a.config, "T": a.T, "E": a.E, "kernel": a.kernel}
+    if a.bench_json:
+        res["build_id"] = line["build_id"]
     for kv in a.match:
         k, v = kv.split("=", 1)
         res[k] = int(v)

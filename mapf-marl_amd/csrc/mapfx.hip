@@ -96,7 +96,7 @@ struct Geo {
   int wpr;
   // LDS regions (byte offsets from the dynamic LDS base)
   int off_map, off_bits, off_oldc, off_newc, off_rc, off_goal, off_rew, off_flag;
-  int map_env_bytes, bits_env_bytes, stage_env_bytes;
+  int map_env_bytes, bits_env_bytes;
   int gen_lds;             // dynamic LDS of a generic-kernel block
   // deferred reward fold of the generic rollout (one env per block): per-agent reward
   // CODES of the last fold_R steps in an LDS ring at off_rew (fold_R = 0: per-step
@@ -110,9 +110,9 @@ struct Geo {
   double step_rew, collide_rew;
   // wave-local fast path (N <= 64: an env never spans two wavefronts)
   int wave_ok, EPW;
-  int wv_off_map, wv_off_dep, wv_off_bits, wv_off_rew, wv_off_stage, wv_lds;
-  int wv_bits_env_bytes, wv_rew_buf, wv_stage_buf, wv_rew_row;  // rew / staging are double-buffered
-  int wv_off_split, wv_split_buf;  // store-wave split: double-buffered per-step output image
+  int wv_off_map, wv_off_dep, wv_off_bits, wv_off_rew, wv_lds;
+  int wv_bits_env_bytes, wv_rew_buf, wv_rew_row;  // the reward rows are double-buffered
+  int wv_off_split, wv_split_ok;  // store-wave split: its LDS starts at wv_off_split
   int wv_fast;                     // build_map_rows_fast applies (W <= 64, pitch % 8 == 0)
   int nblk;                        // grid size of the launch (set in the kernel from its kernargs)
 };
@@ -255,31 +255,17 @@ __device__ __forceinline__ __attribute__((unused)) uint32_t lds_addr(const void*
 #ifndef MAPFX_FOLD_R
 #define MAPFX_FOLD_R 8  // deferred-fold ring depth of the generic rollout (power of two; 0 = off)
 #endif
-#ifndef MAPFX_OCC_U
-#define MAPFX_OCC_U 1   // rows in flight per thread in write_occ16_rows (0: 4 at W <= 5, else 2)
-#endif
 #ifndef MAPFX_EDGE_READLANE
 #define MAPFX_EDGE_READLANE 1  // generic edge scan: the candidate's cells by v_readlane
 #endif
 #ifndef MAPFX_FOLD_PRIO
 #define MAPFX_FOLD_PRIO 3  // s_setprio of the deferred fold's chain (0: none)
 #endif
-#ifndef MAPFX_GEN_CARRY
-// 1: generic rollouts carry each agent's 4 neighbour cells (blocked / occupied bits) from
-// the post-step map of one step to the move decision of the next, and raise an invalid
-// next action's flag one step early (actions prefetched two steps ahead), so a step needs
-// no pre-step map read and no B1.  Measured round 4 at C5 (interleaved, same box): 0.437
-// vs 0.423 ms per T = 64 launch -- slower, so off.
-#define MAPFX_GEN_CARRY 0
-#endif
 #ifndef MAPFX_OCC_GROUPS
 #define MAPFX_OCC_GROUPS 1  // u16 occupancy windows as 8-row groups of 16-byte stores
 #endif
 #ifndef MAPFX_W0_WRITES
 #define MAPFX_W0_WRITES 1  // wave 0 writes window records on the steps without a fold
-#endif
-#ifndef MAPFX_GABL
-#define MAPFX_GABL 0  // diagnostic builds only: generic-kernel parts skipped for timing
 #endif
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations,
@@ -390,7 +376,7 @@ __device__ void write_occ16_rows(const Geo& g, const unsigned char* lds, const i
                                  unsigned char* dst, int nseg, int tid, int nt, int sg_begin = 0) {
   constexpr int NP = (W + 1) / 2;  // cell pairs per row (the last one half used)
   constexpr int h = W / 2;
-  constexpr int U = MAPFX_OCC_U > 0 ? MAPFX_OCC_U : (W <= 5 ? 4 : 2);  // rows in flight per thread
+  constexpr int U = 1;  // rows in flight per thread (2 or 4 measured no faster)
   typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
   const int pitch = g.pitch;
   const bool one_env = g.EPB == 1;
@@ -584,10 +570,8 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   int* rcs = (int*)(lds + g.off_rc) + slot * N;
   int* gls = (int*)(lds + g.off_goal) + slot * N;
   double* rew = (double*)(lds + g.off_rew) + slot * N;  // aliases bitsL (used after the build)
-  // [slot * 4 + {alldone, bad}]: two slots by step parity, three with MAPFX_GEN_CARRY (the
-  // next step's bad-action flag is raised during this step)
+  // [slot * 4 + {alldone, bad}]: two slots by step parity
   int* flag = (int*)(lds + g.off_flag) + slot * 12;
-  constexpr bool CARRY = ROLL && MAPFX_GEN_CARRY != 0;
   // Deferred fold (rollouts, one env per block): every step stores a u16 reward CODE
   // per agent in a ring of FR rows (aliasing rew / the bitmap); every FR-th step (and
   // the last) lanes 0..FR-1 of wave 0 fold one row each -- the same agent-order chain
@@ -626,17 +610,11 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   // actions are loaded one step ahead: step s + 1's load is issued before step s's
   // stores, so waiting for it never waits for them (vmcnt counts both, in order)
   const bool read_act = a.do_step && !a.use_rng;
-  const long long Elong_ = g.E;
-  // CARRY: two steps ahead (act_nx2): step s + 1's action is checked during step s, so
-  // its load must have been issued a whole step earlier
-  int act_nx[APL], act_nx2[APL];
+  int act_nx[APL];
 #pragma unroll
-  for (int k = 0; k < APL; ++k) {
+  for (int k = 0; k < APL; ++k)
     act_nx[k] = (has[k] && read_act)
                     ? load_action(a.actions, a.act_dtype, (long long)env * N + lane + k * g.L) : 4;
-    act_nx2[k] = (CARRY && has[k] && read_act && T > 1)
-                     ? load_action(a.actions, a.act_dtype, (Elong_ + env) * N + lane + k * g.L) : 4;
-  }
   // ---- stage the bitmap, build the padded map, add the agents ----
   if (env_ok) {
     const uint32_t* src =
@@ -662,44 +640,12 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   const int es = (int)sizeof(CellT);  // obs element size == cell size
   const long long Elong = g.E;
 
-  // MAPFX_GEN_CARRY: bit d = neighbour d of the agent's cell blocked (an obstacle nobody
-  // stands on, or outside the grid), bit 4 + d = occupied, on the current (pre-step) map
-  uint32_t nbits[APL];
-  const auto read_nbits = [&](int k) {
-    const int cc = (r[k] + g.P) * g.pitch + c[k] + g.pl;
-    const uint32_t v0 = map[cc - g.pitch], v1 = map[cc + g.pitch], v2 = map[cc - 1], v3 = map[cc + 1];
-    const auto nb = [](uint32_t v, int d) {
-      return (v == CT::OE ? 1u << d : 0u) | ((v & CT::CNT) ? 16u << d : 0u);
-    };
-    return nb(v0, 0) | nb(v1, 1) | nb(v2, 2) | nb(v3, 3);
-  };
-  if constexpr (CARRY) {
-#pragma unroll
-    for (int k = 0; k < APL; ++k) {
-      nbits[k] = has[k] ? read_nbits(k) : 0u;
-      if (has[k] && a.do_step && !a.use_rng && (act_nx[k] < 0 || act_nx[k] > 4))
-        atomicOr(&flag[1], 1);  // step 0's bad action (slot 0)
-    }
-    __syncthreads();  // the neighbour reads before step 0's count moves
-  }
-  int fs = 0;  // CARRY: flag slot of step s (s % 3)
   for (int s = 0; s < T; ++s) {
-    int* fl = flag + (CARRY ? fs : (s & 1)) * 4;
-    const int fs_next = fs == 2 ? 0 : fs + 1;
+    int* fl = flag + (s & 1) * 4;
     int act_in[APL];
 #pragma unroll
     for (int k = 0; k < APL; ++k) act_in[k] = act_nx[k];
-    if constexpr (CARRY) {
-#pragma unroll
-      for (int k = 0; k < APL; ++k) act_nx[k] = act_nx2[k];
-      if (read_act && s + 2 < T) {
-#pragma unroll
-        for (int k = 0; k < APL; ++k)
-          if (has[k])
-            act_nx2[k] = load_action(a.actions, a.act_dtype,
-                                     ((long long)(s + 2) * Elong + env) * N + lane + k * g.L);
-      }
-    } else if (ROLL && read_act && s + 1 < T) {
+    if (ROLL && read_act && s + 1 < T) {
 #pragma unroll
       for (int k = 0; k < APL; ++k)
         if (has[k])
@@ -725,23 +671,16 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         else
           av = act_in[k];
         if (av < 0 || av > 4) {
-          if (!CARRY) atomicOr(&fl[1], 1);  // (CARRY: raised during the previous step)
+          atomicOr(&fl[1], 1);
           av = 4;
         }
         act[k] = av;
         if (!dn[k] && av != 4) {  // __agent_step :319-342
           const int cand =
               oc[k] + (av == 0 ? -g.pitch : (av == 1 ? g.pitch : (av == 2 ? -1 : 1)));
-          bool blocked;
-          int pv;
-          if constexpr (CARRY) {
-            blocked = (nbits[k] >> av) & 1u;
-            pv = (int)((nbits[k] >> (4 + av)) & 1u);  // only pre > 0 is ever asked
-          } else {
-            const uint32_t v = map[cand];
-            blocked = v == CT::OE;
-            pv = (int)(v & CT::CNT);
-          }
+          const uint32_t v = map[cand];
+          const bool blocked = v == CT::OE;
+          const int pv = (int)(v & CT::CNT);
           if (blocked) {
             envc[k] = true;       // out of bounds or free-standing obstacle
           } else {
@@ -754,7 +693,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         newc[ag] = nc[k];
       }
     }
-    if (!CARRY) lds_barrier();  // B1: every pre-step map read is done (and the bad flag)
+    lds_barrier();  // B1: every pre-step map read is done (and the bad flag)
     STAMP(1);
     // ================= P1: move the agent counts =================
     const bool skip = (fl[1] != 0) || !a.do_step;
@@ -775,9 +714,8 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       if constexpr ((FEAT & FEAT_PRIM) != 0) rcs[ag] = (r[k] << 16) | (c[k] & 0xFFFF);
     }
     if (a.do_step && !skip && env_ok) ++tcur;
-    if (lane == 0) {  // the next step's flags: every read of them (step s - 1's, CARRY:
-      // step s - 2's) precedes B1 (CARRY: B3 of step s - 1)
-      int* nf = flag + (CARRY ? fs_next : ((s + 1) & 1)) * 4;
+    if (lane == 0) {  // the next step's flags: every read of them (step s - 1's) precedes B1
+      int* nf = flag + ((s + 1) & 1) * 4;
       nf[0] = 1;
       nf[1] = 0;
     }
@@ -793,7 +731,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     int edgek[APL];
 #pragma unroll
     for (int k = 0; k < APL; ++k) edgek[k] = 0;
-    if (g.L >= 64 && a.do_step && !skip && !(MAPFX_GABL & 8)) {
+    if (g.L >= 64 && a.do_step && !skip) {
       // the env's (old, new) cells, 64 agents per chunk, read once by a wave that
       // has such an i; each i's count is then one ballot popcount per chunk
       constexpr int NCH = APL * 4;  // N <= APL * 256
@@ -871,7 +809,6 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         rew[ag] = 0.0;
       }
       if (!dn[k]) fl[0] = 0;  // every writer stores the same 0: no atomic needed
-      if (MAPFX_GABL & 4) continue;
       if (a.do_step) {
         if (a.node) a.node[ai] = (uint8_t)node;
         if (a.edge) {  // u8 while N <= 256 (edge <= N - 1), else u16 (mapfx_edge_elem_size)
@@ -881,14 +818,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       }
       if (a.traj_pos) ((int2*)a.traj_pos)[ai] = make_int2(r[k], c[k]);
       if (a.traj_done) a.traj_done[ai] = dn[k] ? 1 : 0;
-      if constexpr (CARRY) {
-        // the post-step neighbours: the next step's move decision, and avail (:203-224)
-        nbits[k] = read_nbits(k);
-        if (a.avail) a.avail[ai] = (uint8_t)(16u | (~nbits[k] & 15u));
-        // the next step's action (loaded at this step's start): an invalid one skips its
-        // env (:91-92), raised now so that step needs no barrier before its count moves
-        if (read_act && s + 1 < T && (act_nx[k] < 0 || act_nx[k] > 4)) atomicOr(&flag[fs_next * 4 + 1], 1);
-      } else if (a.avail) {  // :203-224 on the post-step map
+      if (a.avail) {  // :203-224 on the post-step map
         const int cc = nc[k];
         uint32_t m = 16u;
         m |= ((uint32_t)map[cc - g.pitch] != CT::OE) ? 1u : 0u;
@@ -904,7 +834,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       if (a.do_step) {
         if (fl[1] && a.err) atomicCAS(a.err, 0, env + 1);
         double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
-        if (!(MAPFX_GABL & 1) && !FR) {
+        if (!FR) {
           // the adds are one dependent chain; a ring of 8 LDS reads stays in flight
           // ahead of it (the read of reward j + 8 is issued when reward j is added)
           int j = 0;
@@ -941,7 +871,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     const bool fstep = FR && (((s & (FR - 1)) == FR - 1) || s + 1 == T);
     auto fold_ring = [&]() {
       const int s0 = s & ~(FR - 1);
-      if (!env_ok || tid > s - s0 || (MAPFX_GABL & 1)) return;
+      if (!env_ok || tid > s - s0) return;
       // the fold is one dependent chain of N fp64 adds that competes for issue with the
       // other blocks' window writers on its SIMD: it goes first while it runs
       if (MAPFX_FOLD_PRIO) __builtin_amdgcn_s_setprio(MAPFX_FOLD_PRIO);
@@ -1004,7 +934,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     }
     const int wt0 = tail_early ? 64 : 0;  // first writer thread
     STAMP(5);
-    if ((a.obs_window || a.obs_window_occ) && !(MAPFX_GABL & 2) && tid >= wt0) {  // :323-342
+    if ((a.obs_window || a.obs_window_occ) && tid >= wt0) {  // :323-342
       const int wtid = tid - wt0, wnt = g.BT - wt0;
       const int nenv = min(g.EPB, g.E - env0);
       const long long rec0 = (slotE + env0) * (long long)N;  // first record of the block
@@ -1147,18 +1077,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     // B4: the autoreset's map atomics before the next step's reads; without autoreset
     // every hand-off of this step is already ordered by B3 (the tail and the fold read
     // nothing the next step writes before its B1)
-    if (ROLL && s + 1 < T && a.autoreset) {
-      lds_barrier();
-      if constexpr (CARRY) {  // the reset agents' neighbours, then B5 before the count moves
-        if (alldone && a.do_step) {
-#pragma unroll
-          for (int k = 0; k < APL; ++k)
-            if (has[k]) nbits[k] = read_nbits(k);
-        }
-        lds_barrier();
-      }
-    }
-    fs = fs_next;
+    if (ROLL && s + 1 < T && a.autoreset) lds_barrier();
   }
 
   // ---- write back the env state ----
@@ -1190,12 +1109,6 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
 //   agent order; the wave writes the staged records with 16-byte stores.
 // Actions for step s+1 are loaded while step s runs.  All offsets are 32-bit.
 // ===========================================================================
-#ifndef MAPFX_DIRECT_REC
-#define MAPFX_DIRECT_REC 1
-#endif
-#ifndef MAPFX_ABLATE
-#define MAPFX_ABLATE 0  // diagnostic builds only: bit mask of parts skipped for timing
-#endif
 #ifdef MAPFX_CLOCKS
 // Diagnostic build only: per-wave shader-clock / 100 MHz real-time clock at the
 // start and end of the step loop, read back with mapfx_debug_clocks().
@@ -1289,7 +1202,7 @@ __device__ inline void build_map_rows_fast(const Geo& g, uint32_t* map32, const 
       hi = (uint32_t)(rb >> (64 - pl)) | (e <= 64 ? ~0u : (e < 96 ? ~0u << (e - 64) : 0u));
     }
     uint2* row2 = (uint2*)(map32 + pr * wpr);
-    uint2* row2b = map32b ? (uint2*)(map32b + pr * wpr) : nullptr;  // (a second copy: MAPFX_SPLIT_DBM)
+    uint2* row2b = map32b ? (uint2*)(map32b + pr * wpr) : nullptr;  // (the split's second count map)
 #pragma unroll
     for (int j = 0; j < MAXW / 2; ++j) {
       if (2 * j < wpr) {
@@ -1549,137 +1462,41 @@ __device__ __forceinline__ void stage_occ_record(const uint32_t (&R)[(WIN * WIN 
 }
 
 // ---- store-wave split (runner rollout, N = 16) --------------------------------
-// The wave that steps the envs (the "step wave") keeps only the dependency chain
-// of a step: moves, LDS count atomics, edge collisions (a cross-lane scan) and
-// the dones.  For every agent it hands a 16-byte "info" word (new cell, carried
-// neighbour bytes, flags, edge count, t) and its raw post-step window rows to a
-// second wave of the workgroup (the "store wave") through a double-buffered LDS
-// image.  The store wave derives every output from them -- window record, node
-// collision, avail mask, (row, col), the fp64 reward and its agent-order fold --
-// and writes all of it to HBM (records through an LDS image with lane-contiguous
-// 16-byte stores).  One workgroup barrier per step hands an image over: the step
-// wave fills image s & 1 with step s-1 during step s, while the store wave
-// drains image (s-1) & 1.  The chip then carries two waves per SIMD, and the
-// step wave issues no global store inside its loop.
+// A workgroup is three waves.  The "step wave" keeps only the
+// dependency chain of a step: moves, LDS count atomics, edge collisions (a cross-lane
+// scan) and the dones.  It keeps TWO agent-count maps: map s & 1 holds the counts
+// after step s (each step moves an agent's count in that map from where it stood after
+// step s - 2 to its new cell), so a step's map stays intact for the whole next barrier
+// interval and the store waves read that step's window rows from it themselves.  Per
+// agent the step wave hands over a 16-byte info word (new cell, the 4 neighbour bytes,
+// flags, t) and, one step later, its edge count.  Two "store waves" take the steps in
+// turn (even / odd) and spread each over two barrier intervals: a(q) builds the window
+// record (SWAR) and stages it in the wave's LDS image, b(q) stores it with
+// lane-contiguous 16-byte stores together with node / edge / avail / done / (row, col) /
+// t / term, and every 16th step folds the fp64 rewards of 16 steps x 4 envs from
+// per-agent reward codes.  One barrier per step (LDS traffic only), so the step wave
+// issues no global store inside its loop and the stores stay in flight across barriers.
+// Measured alternatives (a 2-wave form, a single image of raw window rows, a 3-slot ring
+// published a barrier late, a MOVE / MAP step side, nontemporal stores) were slower and
+// are gone from the source; their numbers are in DESIGN.md §4.1b.
 #ifndef MAPFX_SPLIT
 #define MAPFX_SPLIT 1  // store-wave split for the N = 16 runner rollout
 #endif
-#ifndef MAPFX_SPLIT_NT
-// 1: nontemporal stores from the store waves.  Round 3 (C2, rollout T sweep):
-// plain stores take T = 64 from 71 to 55-57 us and leave T = 20 unchanged.
-#define MAPFX_SPLIT_NT 0
-#endif
-#ifndef MAPFX_SPLIT_ALT
-// 1: two store waves that take the steps in turn (even / odd), each spreading its
-// step over two barrier intervals (ROLE_ALT); 0: one store wave per step
-#define MAPFX_SPLIT_ALT 1
-#endif
-#ifndef MAPFX_SPLIT_MOVE
-// 1 (with ALT): the step side is two waves -- a MOVE wave that runs the dynamics from
-// the static obstacle flags and a MAP wave that keeps the agent-count map and builds
-// the step images -- whenever no agent stands, or is reset, on an obstacle (then a
-// move is refused exactly on obstacle / border cells, mapf_gridworld.py:319-342);
-// otherwise the block runs the one-wave step side (wave 1 idles).  Measured round 3
-// at C2: the step side alone 0.65 -> 0.57 us/step, but the kernel is bound by its
-// store side (T = 20: 23.2 vs 23.0 us, T = 64: 57.4 vs 55.4 us with plain stores),
-// so the three-wave split stays the default.
-#define MAPFX_SPLIT_MOVE 0
-#endif
-#ifndef MAPFX_SPLIT_WAVES
-#define MAPFX_SPLIT_WAVES (MAPFX_SPLIT_MOVE ? 4 : MAPFX_SPLIT_ALT ? 3 : 2)  // 3 without ALT: record wave + small-output wave
-#endif
-#ifndef MAPFX_SPLIT_LAG
-// 1 (ALT only): the step images are a 3-slot ring published one barrier late.  The step
-// wave writes step q's image in iteration q + 1 and the store waves read it after barrier
-// q + 3, so the step wave's barrier waits for everything but its own latest image writes
-// (s_waitcnt lgkmcnt(NQ)): the image stores of a step leave its critical path.  Measured
-// round 4 (C2, same box, interleaved): T = 20 23.3 vs 23.0 us, T = 64 54.4 vs 53.5 us --
-// slower (one more barrier interval of drain, 4 KB more LDS per block), so off.  Cutting
-// the image to one store per lane (diagnostic ablation 2048) had measured -1.4 us: the
-// image's LDS traffic costs, not the step wave's wait for it.
-#define MAPFX_SPLIT_LAG 0
-#endif
-constexpr int SPLIT_NIMG = MAPFX_SPLIT_LAG ? 3 : 2;  // step images in the ring
-#ifndef MAPFX_SPLIT_DBM
-// 1 (ALT, no LAG / MOVE): two agent-count maps, M0 for even steps and M1 for odd ones.
-// Step s moves the counts of map s & 1 from the positions after step s - 2 to those after
-// step s, so a step's map stays intact for the whole next barrier interval: the store
-// waves read a step's window rows from it themselves, and the step wave hands over only
-// a 16-byte info word per agent (and its edge count one step later) instead of the info
-// word plus the raw window rows (round 4: the step wave's image stores cost ~1.4 us of a
-// C2 T = 20 launch).  The step wave reads the 4 neighbour bytes of its
-// agent's new cell, not its 5 window rows.
-#define MAPFX_SPLIT_DBM (MAPFX_SPLIT_ALT && !MAPFX_SPLIT_LAG && !MAPFX_SPLIT_MOVE)
-#endif
-constexpr int SPLIT_DBM_INFO = 2 * 64 * 16;  // DBM: info words of two steps
-constexpr int SPLIT_DBM_EDGE = 2 * 64;       // DBM: edge counts of two steps
-// step-side waves ahead of the store waves
-#define MAPFX_SPLIT_SW0 (MAPFX_SPLIT_MOVE ? 2 : 1)
-constexpr int SPLIT_RING_LDS = 2 * 64 * 16;  // MOVE -> MAP ring: 2 steps x 64 lanes x u32x4
-
-// `sum(rewards)` (mapf_gridworld.py:141) over a 16-lane DPP row: a naive left fold
-// ((0 + r_0) + r_1) + ... in agent order.  Iteration k makes lane k's running sum
-// final (each lane adds its own reward to its left neighbour's running sum), so
-// after 15 shifts lane j holds the fold of agents 0..j; lane 0's left input is
-// the bound-control zero, i.e. the fold's initial 0.
-__device__ __forceinline__ double row_fold16(double r) {
-  double R = 0.0 + r;
-#pragma unroll
-  for (int k = 1; k < 16; ++k) {
-    const uint64_t b = (uint64_t)__double_as_longlong(R);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x111, 0xF, 0xF, true);  // row_shr:1
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x111, 0xF, 0xF, true);
-    R = __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo)) + r;
-  }
-  return R;
-}
-
-
-template <int WIN, int LL>
-struct SplitLayout {
-  static constexpr int REC = 2 * WIN * WIN;             // window record bytes per agent
-  static constexpr int NXW = (WIN > 5 ? 3 : 2) * WIN;  // raw row words per agent
-  static constexpr int SLOT = (4 + NXW + 3) / 4 * 16;   // info u32x4 + raw rows, per agent,
-                                                        // stored chunk-major (bank-conflict free)
-  static constexpr int BYTES = 64 * SLOT;               // one image (64 agents)
-  static constexpr int STORE_LDS = 2 * 64 * REC;       // staged-record images of the output side
-  static_assert(LL == 16, "4 envs of 16 agents per wave");
-};
-#ifndef MAPFX_SPLIT_SOA
-#define MAPFX_SPLIT_SOA 1  // slot images chunk-major: chunk i of lane l at (64 i + l) * 16
-#endif
-// byte stride between lanes / u32x4 stride between one lane's chunks in a slot image
-#define SLOT_LANE (MAPFX_SPLIT_SOA ? 16 : SplitLayout<WIN, LL>::SLOT)
-#define SLOT_CHUNK (MAPFX_SPLIT_SOA ? 64 : 1)
+constexpr int SPLIT_WAVES = 3;               // step wave + two store waves
+constexpr int SPLIT_DBM_INFO = 2 * 64 * 16;  // info words of two steps
+constexpr int SPLIT_DBM_EDGE = 2 * 64;       // edge counts of two steps
+constexpr int SPLIT_FOLD_LDS = 256 * 8 + 32 * 64;  // reward-code table + 32-step code ring
 
 // info.z flag bits
 constexpr uint32_t SF_DONE = 1, SF_LIVE = 2, SF_DNOLD = 4, SF_ENVC = 8, SF_SKIP = 16, SF_ALLDONE = 64;
 
 // Workgroup barrier that waits for this wave's LDS traffic only: outstanding
 // global stores stay in flight (a __syncthreads() would drain them every step).
-__device__ __forceinline__ void split_barrier() {
-  if (MAPFX_ABLATE & 1024) return;  // diagnostic only: no hand-over (results are garbage)
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-// The step wave's barrier under MAPFX_SPLIT_LAG: every LDS operation but the NQ most
-// recent (this iteration's image stores, which nobody reads before the NEXT barrier) has
-// completed.  LDS operations of a wave complete in order, and an iteration issues more
-// than NQ of them after the previous iteration's image stores, so those are complete;
-// an outstanding scalar load only makes the wait stricter.
-template <int NQ>
-__device__ __forceinline__ void split_barrier_lag() {
-  static_assert(NQ >= 0 && NQ < 16, "lgkmcnt");
-  if (MAPFX_ABLATE & 1024) return;
-  asm volatile("s_waitcnt lgkmcnt(%0)\n\ts_barrier" ::"n"(NQ) : "memory");
-}
+__device__ __forceinline__ void split_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <typename P, typename V>
 __device__ __forceinline__ void split_store(P p, V v) {
-  // diagnostic ablation 512: the store waves compute everything but store nothing (a
-  // grid-size test the compiler cannot fold keeps the values live)
-  if ((MAPFX_ABLATE & 512) && blockIdx.x != 0x7FFFFFF0u) return;
-  if (MAPFX_SPLIT_NT) __builtin_nontemporal_store(v, p);
-  else *p = v;
+  *p = v;
 }
 
 // padded LDS cell index -> (row, col); cell < 2^16, pitch < 256
@@ -1689,206 +1506,8 @@ __device__ __forceinline__ int2 padded_cell_rc(const Geo& g, int cell) {
   return make_int2((int)pr - g.P, cell - (int)pr * g.pitch - g.pl);
 }
 
-// Output side of the split.  ROLE_ALL: one store wave does everything (2-wave
-// workgroups); with MAPFX_SPLIT_WAVES == 3 a "record wave" (ROLE_REC: window
-// records) and a "small wave" (ROLE_SMALL: node / edge / avail / done / (row, col),
-// fp64 reward fold, t, term) share the work.  Both read the step wave's image
-// after the barrier that hands it over.
-//   records: SWAR planes from the raw rows, staged in the wave's own LDS image
-//     and written one step later with lane-contiguous 16-byte stores (the
-//     staged step q-1 is read together with step q's image: one LDS round trip
-//     per step);
-//   small outputs: derived from the info word and the centre row; the reward
-//     fold is an in-row DPP scan (row_fold16), lane LL-1 of each env stores it.
-constexpr int ROLE_ALL = 0, ROLE_REC = 1, ROLE_SMALL = 2;
-constexpr int SPLIT_FOLD_LDS = 256 * 8 + 32 * 64;  // ALT reward table + code ring
 
-// ROLE_ALT (MAPFX_SPLIT_ALT): store wave `par` takes the steps q with q % 2 == par.
-// The step wave publishes step q's image at barrier q + 2 (image (q + 1) & 1, not
-// rewritten before barrier q + 3).  Interval q + 2 .. q + 3 ("a"): read the image,
-// build the record and stage it in the wave's own LDS image, keep the info word and
-// the node flag, put the agents' reward codes in the ring; interval q + 3 .. q + 4
-// ("b"): read the staged record back, store it with lane-contiguous 16-byte stores,
-// derive and store the per-agent and per-env outputs, and every 16th step fold the
-// rewards of the 16 steps.  Each store wave thus carries half a step of work per
-// barrier interval, and the block has three waves whose chains overlap.  The block's
-// throughput is VALU issue (its three waves share one SIMD's worth of issue per step),
-// so instructions are what this path saves.
-template <int WIN, int LL, bool OCC>
-__device__ __forceinline__ void split_store_wave_alt(const Geo& g, const Args& a, unsigned char* sp,
-                                                     unsigned char* own, double* rtab, unsigned char* codes,
-                                                     int env0, int lane, int par) {
-  typedef __attribute__((address_space(1))) unsigned char gbyte;
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  typedef int i32x2 __attribute__((ext_vector_type(2)));
-  using SL = SplitLayout<WIN, LL>;
-  constexpr int H2 = WIN / 2, REC = OCC ? WIN * WIN : SL::REC, NQ = SL::SLOT / 16;
-  constexpr int RCH = 4 * REC;                  // 16-byte chunks of the wave's 64 records
-  constexpr int NRC = (RCH + 63) / 64;
-  const int T = a.T;
-  const uint32_t E = (uint32_t)g.E, EN = E * (uint32_t)LL;
-  const int slot = lane / LL, ag = lane % LL;
-  const uint32_t env = (uint32_t)(env0 + slot), ag0 = (uint32_t)env0 * LL;
-  const u32x4* ost = (const u32x4*)__builtin_assume_aligned(own, 16);
-  uint32_t k_nc = 0, k_nb = 0, k_fl = 0, k_t = 0, k_node = 0;  // step q's info, kept from a to b
-
-  // Rewards: an agent's reward (:94-130) is a function of five small fields, so the
-  // a part stores one CODE byte per agent (bit 0 node, bits 1-3 the SF_LIVE / SF_DNOLD
-  // / SF_ENVC flags, bits 4-7 edge; N == 16 bounds edge by 15) in a 32-step ring, and
-  // `sum(rewards)` (:141) of 16 steps x 4 envs is folded at once, one (env, step) per
-  // lane, from a table of the 256 code rewards: 16 fp64 adds per 16 steps instead of a
-  // 15-add DPP row scan per step.
-  for (int c = lane + 64 * par; c < 256; c += 128) {  // the table (both waves, before barrier 1)
-    double rr = 0.0;  // exact fp64 op order of the reference
-    if (c & SF_LIVE) {
-      if (!(c & SF_DNOLD)) {
-        if (c & SF_ENVC) rr = rr + g.collide_rew;
-        rr = rr + g.step_rew;
-      }
-      rr = rr + g.collide_rew * (double)(c & 1);
-      rr = rr + g.collide_rew * (double)(c >> 4);
-    }
-    rtab[c] = rr;
-  }
-  // steps q0 .. q0 + cnt - 1 (one 16-step batch of the ring): lane = (env e, step j)
-  auto fold_batch = [&](uint32_t q0, int cnt) {
-    const int j = lane & 15, e = lane >> 4;
-    if (j < cnt) {
-      const u32x4 cv = *(const u32x4*)__builtin_assume_aligned(codes + ((q0 + j) & 31) * 64 + e * 16, 16);
-      const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w};
-      double v[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = rtab[(cw[i >> 2] >> (8 * (i & 3))) & 0xFFu];
-      double R = 0.0;  // the naive left fold in agent order
-#pragma unroll
-      for (int i = 0; i < 16; ++i) R = R + v[i];
-      const uint32_t ei = (q0 + j) * E + (uint32_t)env0 + e;
-      split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), R);
-      if (a.reward_f32) a.reward_f32[ei] = (float)R;
-    }
-  };
-
-  auto part_b = [&](uint32_t q) {
-    u32x4 rv[NRC];
-#pragma unroll
-    for (int k = 0; k < NRC; ++k)
-      rv[k] = (MAPFX_ABLATE & 32768) ? u32x4{q, (uint32_t)lane, (uint32_t)k, 0u}  // diagnostic: no LDS read
-                                     : ost[(k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0];
-    gbyte* rec = (gbyte*)(OCC ? a.obs_window_occ : a.obs_window) + (q * EN + ag0) * (uint32_t)REC;
-#pragma unroll
-    for (int k = 0; k < NRC; ++k)
-      if ((k < NRC - 1 || lane + 64 * k < RCH) && (!(MAPFX_ABLATE & 16384) || blockIdx.x == 0x7FFFFFF0u))
-        split_store((__attribute__((address_space(1))) u32x4*)(rec + 16u * (lane + 64 * k)), rv[k]);
-    const uint32_t fl = k_fl;
-    const uint32_t nzn = (((k_nb & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
-    const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
-    const uint32_t edge = fl >> 8, node = k_node;
-    const uint32_t ai = q * EN + ag0 + lane;
-    const int2 rc = padded_cell_rc(g, (int)k_nc);
-    split_store((__attribute__((address_space(1))) i32x2*)((gbyte*)a.traj_pos + 8u * ai), i32x2{rc.x, rc.y});
-    split_store((gbyte*)a.node + ai, (unsigned char)node);
-    split_store((gbyte*)a.edge + ai, (unsigned char)edge);
-    split_store((gbyte*)a.avail + ai, (unsigned char)availm);
-    split_store((gbyte*)a.traj_done + ai, (unsigned char)(fl & SF_DONE));
-    if (ag == LL - 1) {
-      const uint32_t ei = q * E + env;
-      split_store((__attribute__((address_space(1))) int*)((gbyte*)a.traj_t + 4u * ei), (int)k_t);
-      split_store((gbyte*)a.term + ei, (unsigned char)((fl & SF_ALLDONE) ? 1 : 0));
-      if (a.err && (fl & SF_SKIP)) atomicCAS(a.err, 0, (int)env + 1);
-    }
-    // the batch ends here: every code of it is in the ring (this wave's a(q) one
-    // interval ago, the other wave's a(q - 1) before the last barrier)
-    if ((q & 15u) == 15u || q + 1 == (uint32_t)T) fold_batch(q & ~15u, (int)(q & 15u) + 1);
-  };
-
-  // MAPFX_SPLIT_LAG: step q's image is complete at barrier q + 3 (ring slot q % 3), one
-  // barrier later than without it (barrier q + 2, buffer (q + 1) & 1)
-  constexpr int LAGS = MAPFX_SPLIT_LAG ? 1 : 0;
-  const int rounds = T > 0 ? T + 1 + LAGS : 0;
-  int islot = 0;  // LAG: ring slot of the image read next
-  for (int s = 1; s <= rounds; ++s) {
-#ifdef MAPFX_STAMPS  // diagnostic: end of round s - 1's work (columns 5 / 7 of row s - 1)
-    if (s > 1) {
-      unsigned long long t_;
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
-      if (blockIdx.x == 0 && lane == 0 && s - 1 < 256) g_stamps[(s - 1) * 8 + 5 + 2 * par] = t_;
-    }
-#endif
-    split_barrier();
-    if (s <= 1 + LAGS || (MAPFX_ABLATE & 256)) continue;
-    const int q = s - 2 - LAGS;
-    const int qslot = MAPFX_SPLIT_LAG ? islot : ((s - 1) & 1);
-    if (MAPFX_SPLIT_LAG) islot = islot == SPLIT_NIMG - 1 ? 0 : islot + 1;
-    if ((q & 1) == par) {  // a(q)
-      const u32x4* sl = (const u32x4*)__builtin_assume_aligned(
-          sp + qslot * g.wv_split_buf + lane * SLOT_LANE, 16);
-      uint32_t w[4 * NQ];
-#pragma unroll
-      for (int i = 0; i < NQ; ++i) {
-        // diagnostic 65536: one LDS read of the image (the info chunk) instead of NQ
-        const u32x4 v = sl[(MAPFX_ABLATE & 65536) ? 0 : SLOT_CHUNK * i];
-        w[4 * i] = v.x ^ ((MAPFX_ABLATE & 65536) ? (uint32_t)i : 0u);
-        w[4 * i + 1] = v.y;
-        w[4 * i + 2] = v.z;
-        w[4 * i + 3] = v.w;
-      }
-      if (MAPFX_ABLATE & 262144) {  // diagnostic: the window rows read from the cell map
-        extern __shared__ __align__(16) unsigned char lds_[];
-        const uint32_t* m32 = (const uint32_t*)(lds_ + g.wv_off_map + slot * g.map_env_bytes);
-        const int w0 = ((int)(w[0] & 0xFFFFu) - H2 * g.pitch - H2) >> 2, wpr = g.pitch >> 2;
-#pragma unroll
-        for (int y = 0; y < WIN; ++y) {
-          w[4 + y] = m32[w0 + y * wpr];
-          w[4 + WIN + y] = m32[w0 + y * wpr + 1];
-        }
-      }
-      const uint32_t* qx = w + 4;
-      const int o = ((int)w[0] - H2) & 3;
-      if constexpr (OCC) {
-        uint32_t R[(WIN * WIN + 3) / 4 + 1];
-        occ_words<WIN>(qx, o, R);
-        stage_occ_record<WIN>(R, lds_addr(own + lane * REC));
-      } else if (MAPFX_ABLATE & 4096) {  // diagnostic: the staging writes of raw words (no VALU)
-        typedef __attribute__((address_space(3))) uint32_t lds_u32;
-        typedef __attribute__((address_space(3))) uint16_t lds_u16;
-        const uint32_t ra = lds_addr(own + lane * REC);
-        lds_u32* d = (lds_u32*)(uintptr_t)(ra + (ra & 2));
-#pragma unroll
-        for (int j = 0; j < (REC - 2) / 4; ++j) d[j] = qx[j % (2 * WIN)];
-        *(lds_u16*)(uintptr_t)(ra + ((ra & 2) ? 0 : REC - 2)) = (uint16_t)qx[0];
-      } else if (MAPFX_ABLATE & 8192) {  // diagnostic: the record's VALU, one LDS write
-        typedef __attribute__((address_space(3))) uint16_t lds_u16;
-        uint32_t R[4 * WIN];
-        window_regs<WIN>(qx, o, R);
-        constexpr int NW = (REC + 3) / 4;
-        uint32_t wv[NW];
-        rec_words<WIN>(R, wv, std::make_integer_sequence<int, NW>{});
-        uint32_t x = 0;
-#pragma unroll
-        for (int j = 0; j < NW; ++j) x ^= __builtin_amdgcn_alignbyte(wv[(j + 1) % NW], wv[j], (lane & 1) * 2);
-        *(lds_u16*)(uintptr_t)lds_addr(own + lane * REC) = (uint16_t)x;
-      } else {
-        uint32_t R[4 * WIN];
-        window_regs<WIN>(qx, o, R);
-        stage_record<WIN>(R, own + lane * REC);
-      }
-      // node collision (:344-362): post-step count = c - 1 + obstacle >= 2 (centre cell)
-      const uint32_t ctr = (__builtin_amdgcn_alignbyte(qx[WIN + H2], qx[H2], o) >> (8 * H2)) & 0xFFu;
-      k_node = ((ctr & 0x7Fu) + (ctr >> 7) >= 3u && !(w[2] & SF_SKIP)) ? 1u : 0u;
-      k_nc = w[0], k_nb = w[1], k_fl = w[2], k_t = w[3];
-      codes[(q & 31) * 64 + lane] =
-          (unsigned char)(k_node | (k_fl & (SF_LIVE | SF_DNOLD | SF_ENVC)) | ((k_fl >> 4) & 0xF0u));
-    } else if (q >= 1) {   // b(q - 1)
-      part_b((uint32_t)(q - 1));
-    }
-  }
-  if (T > 0 && ((T - 1) & 1) == par && !(MAPFX_ABLATE & 256)) {  // the last step's b part
-    wave_fence();
-    part_b((uint32_t)(T - 1));
-  }
-}
-
-// The store waves under MAPFX_SPLIT_DBM.  Wave `par` takes the steps q with q % 2 == par:
+// The two store waves.  Wave `par` takes the steps q with q % 2 == par:
 //   a(q), the interval after barrier q + 1: step q's info word (written by the step wave
 //     in its iteration q) and the agent's window rows read from map q & 1 -- intact until
 //     the step wave's iteration q + 2 moves that map's counts again -- to the record, staged
@@ -2018,124 +1637,9 @@ __device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a
     }
 #endif
     split_barrier();
-    if (MAPFX_ABLATE & 256) continue;
     const int q = s - 1;  // a(q) now; b(q - 1) by the other parity
     if (q < T && (q & 1) == par) part_a((uint32_t)q);
     else if (q >= 1 && ((q - 1) & 1) == par) part_b((uint32_t)(q - 1));
-  }
-}
-
-template <int WIN, int LL, int ROLE, bool OCC = false>
-__device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, unsigned char* sp,
-                                                 unsigned char* own, int env0, int lane) {
-  typedef __attribute__((address_space(1))) unsigned char gbyte;  // global_store, not flat_
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  typedef int i32x2 __attribute__((ext_vector_type(2)));
-  using SL = SplitLayout<WIN, LL>;
-  constexpr bool RECS = ROLE != ROLE_SMALL, SMALL = ROLE != ROLE_REC;
-  // OCC: obs_window_occ records (WIN*WIN bytes, one occupancy plane), else obs_window
-  constexpr int H2 = WIN / 2, REC = OCC ? WIN * WIN : SL::REC, NQ = SL::SLOT / 16;
-  constexpr int RCH = 4 * REC;                  // 16-byte chunks of the wave's 64 records
-  constexpr int NRC = (RCH + 63) / 64;          // chunk rounds per lane
-  constexpr int IMG = 64 * REC;                 // one staged-record image
-  const int T = a.T;
-  const uint32_t E = (uint32_t)g.E, EN = E * (uint32_t)LL;
-  const int slot = lane / LL, ag = lane % LL;
-  const uint32_t env = (uint32_t)(env0 + slot), ag0 = (uint32_t)env0 * LL;
-  const u32x4* ost = (const u32x4*)__builtin_assume_aligned(own, 16);
-
-  // staged records of step p (image p & 1): read / store
-  auto read_recs = [&](uint32_t p, u32x4 (&rv)[NRC]) {
-#pragma unroll
-    for (int k = 0; k < NRC; ++k)
-      rv[k] = ost[(p & 1) * (IMG / 16) + ((k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0)];
-  };
-  auto store_recs = [&](uint32_t p, const u32x4 (&rv)[NRC], bool ok) {
-    gbyte* rec = (gbyte*)(OCC ? a.obs_window_occ : a.obs_window) + (p * EN + ag0) * (uint32_t)REC;
-#pragma unroll
-    for (int k = 0; k < NRC; ++k)
-      if (ok && (k < NRC - 1 || lane + 64 * k < RCH))
-        split_store((__attribute__((address_space(1))) u32x4*)(rec + 16u * (lane + 64 * k)), rv[k]);
-  };
-
-  const int rounds = T > 0 ? T + 1 : 0;
-  for (int s = 1; s <= rounds; ++s) {
-    split_barrier();
-    if (s == 1 || (MAPFX_ABLATE & 256)) continue;
-    const uint32_t q = (uint32_t)(s - 2);  // the step image (s - 1) & 1 carries
-    const u32x4* sl = (const u32x4*)__builtin_assume_aligned(
-        sp + ((s - 1) & 1) * g.wv_split_buf + lane * SLOT_LANE, 16);
-    uint32_t w[4 * NQ];
-#pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-      const u32x4 v = sl[SLOT_CHUNK * i];
-      w[4 * i] = v.x;
-      w[4 * i + 1] = v.y;
-      w[4 * i + 2] = v.z;
-      w[4 * i + 3] = v.w;
-    }
-    u32x4 rv[NRC];
-    if constexpr (RECS) read_recs(q - 1, rv);  // q = 0: stale image, nothing of it is stored
-    const int nc = (int)w[0];
-    const uint32_t nb = w[1], fl = w[2];
-    const uint32_t* qx = w + 4;
-    const int o = (nc - H2) & 3;
-    if constexpr (RECS && OCC) {
-      uint32_t R[(WIN * WIN + 3) / 4 + 1];
-      occ_words<WIN>(qx, o, R);
-      store_recs(q - 1, rv, q > 0);
-      stage_occ_record<WIN>(R, lds_addr(own + (q & 1) * IMG + lane * REC));
-    } else if constexpr (RECS) {
-      uint32_t R[4 * WIN];
-      window_regs<WIN>(qx, o, R);
-      store_recs(q - 1, rv, q > 0);
-      stage_record<WIN>(R, own + (q & 1) * IMG + lane * REC);
-    }
-    if constexpr (SMALL) {
-      // node collision (:344-362): post-step count = c - 1 + obstacle >= 2 (centre cell)
-      const uint32_t ctr = (__builtin_amdgcn_alignbyte(qx[WIN + H2], qx[H2], o) >> (8 * H2)) & 0xFFu;
-      uint32_t node = (ctr & 0x7Fu) + (ctr >> 7) >= 3u ? 1u : 0u;
-      if (fl & SF_SKIP) node = 0;
-      // avail (:203-224): a neighbour is available iff its c != 0; stay always
-      const uint32_t nzn = (((nb & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
-      const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
-      const uint32_t edge = fl >> 8;
-      // reward (:94-130, exact fp64 op order)
-      double rr = 0.0;
-      if (fl & SF_LIVE) {
-        if (!(fl & SF_DNOLD)) {
-          if (fl & SF_ENVC) rr = rr + g.collide_rew;
-          rr = rr + g.step_rew;
-        }
-        rr = rr + g.collide_rew * (double)node;
-        rr = rr + g.collide_rew * (double)edge;
-      }
-      const uint32_t ai = q * EN + ag0 + lane;
-      const int2 rc = padded_cell_rc(g, nc);
-      split_store((__attribute__((address_space(1))) i32x2*)((gbyte*)a.traj_pos + 8u * ai),
-                  i32x2{rc.x, rc.y});
-      split_store((gbyte*)a.node + ai, (unsigned char)node);
-      split_store((gbyte*)a.edge + ai, (unsigned char)edge);
-      split_store((gbyte*)a.avail + ai, (unsigned char)availm);
-      split_store((gbyte*)a.traj_done + ai, (unsigned char)(fl & SF_DONE));
-      const double Rs = row_fold16(rr);  // `sum(rewards)` (:141): lane LL-1 holds the total
-      if (ag == LL - 1) {
-        const uint32_t ei = q * E + env;
-        split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), Rs);
-        split_store((__attribute__((address_space(1))) int*)((gbyte*)a.traj_t + 4u * ei), (int)w[3]);
-        split_store((gbyte*)a.term + ei, (unsigned char)((fl & SF_ALLDONE) ? 1 : 0));
-        if (a.reward_f32) a.reward_f32[ei] = (float)Rs;
-        if (a.err && (fl & SF_SKIP)) atomicCAS(a.err, 0, (int)env + 1);
-      }
-    }
-  }
-  if constexpr (RECS) {
-    if (T > 0 && !(MAPFX_ABLATE & 256)) {  // the last step's staged records
-      wave_fence();
-      u32x4 rv[NRC];
-      read_recs((uint32_t)(T - 1), rv);
-      store_recs((uint32_t)(T - 1), rv, true);
-    }
   }
 }
 
@@ -2172,17 +1676,17 @@ __device__ __forceinline__ void split_store_wave(const Geo& g, const Args& a, un
 // block stays faster (52.7 vs 57.0 us; tools/gpucmd_r04q.sh)
 template <int WIN, bool ROLL, bool FULLW, bool RUNNER, int LL, bool SPLIT = false, bool OCC = false, int ABT = 0>
 // (split: 4 blocks per CU must be resident -- one wave per SIMD of each role -- so the
-// register budget is that of MAPFX_SPLIT_WAVES waves per SIMD)
-__global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? MAPFX_SPLIT_WAVES : 1)
+// register budget is that of SPLIT_WAVES waves per SIMD)
+__global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_WAVES : 1)
     mapf_wave_kernel(MAPFX_HOT_PARAMS, Args a0, Geo g0) {
   Args a = a0;
   Geo g = g0;
   MAPFX_HOT_APPLY(a, g);
   extern __shared__ __align__(16) unsigned char lds[];
   static_assert(!SPLIT || (ROLL && FULLW && RUNNER && LL == 16 && WIN > 0), "split: runner rollout, N = 16");
-  static_assert(!OCC || (SPLIT && (MAPFX_SPLIT_ALT || MAPFX_SPLIT_WAVES == 2)), "occupancy records: one store wave or ALT");
+  static_assert(!OCC || SPLIT, "occupancy records: the split's store waves");
   if constexpr (SPLIT) {
-    if (threadIdx.x >= 64 * MAPFX_SPLIT_SW0) {  // the output side of the split
+    if (threadIdx.x >= 64) {  // the output side of the split
       if (MAPFX_PRIO_STORE) __builtin_amdgcn_s_setprio(MAPFX_PRIO_STORE);
       const int e0 = xcd_block(blockIdx.x, g.nblk) * (64 / LL);
       if (g.wv_fast) {  // the store waves build their share of the padded maps (rows
@@ -2192,38 +1696,26 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
         const uint32_t* src = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)(e0 + sl) * g.map_stride));
         uint32_t pf[1][3];
         const int bl = l64 % LL + LL * (threadIdx.x >> 6);
-        fast_row_prefetch<1>(g, src, bl, LL * MAPFX_SPLIT_WAVES, pf);
+        fast_row_prefetch<1>(g, src, bl, LL * SPLIT_WAVES, pf);
         build_map_rows_fast<MAPFX_FAST_WPR, 1>(g, (uint32_t*)(lds + g.wv_off_map + sl * g.map_env_bytes), src,
-                                               bl, LL * MAPFX_SPLIT_WAVES, pf,
-                                               MAPFX_SPLIT_DBM ? (uint32_t*)(lds + g.wv_off_split + sl * g.map_env_bytes)
-                                                               : nullptr);
+                                               bl, LL * SPLIT_WAVES, pf,
+                                               (uint32_t*)(lds + g.wv_off_split + sl * g.map_env_bytes));
       }
       split_barrier();
-      unsigned char* sp = lds + g.wv_off_split;
-      unsigned char* own = sp + SPLIT_NIMG * g.wv_split_buf;
       constexpr int RECB = OCC ? WIN * WIN : 2 * WIN * WIN;  // one wave's staged image: 64 * RECB
-      double* rtab = (double*)(own + 2 * 64 * RECB);          // ALT: reward table + code ring
-      const int par = (int)(threadIdx.x >> 6) - MAPFX_SPLIT_SW0;  // ALT: this wave's step parity
-      if (MAPFX_SPLIT_DBM) {  // [M1: 64 / LL maps][info: 2 steps][edge: 2 steps][staged records][fold]
-        unsigned char* m1 = lds + g.wv_off_split;
-        unsigned char* inf = m1 + (64 / LL) * g.map_env_bytes;
-        unsigned char* eri = inf + SPLIT_DBM_INFO;
-        unsigned char* ownd = eri + SPLIT_DBM_EDGE;
-        double* rt = (double*)(ownd + 2 * 64 * RECB);
-        split_store_wave_dbm<WIN, LL, OCC>(g, a, lds + g.wv_off_map, m1, inf, eri, ownd + par * 64 * RECB, rt,
-                                           (unsigned char*)(rt + 256), e0, threadIdx.x & 63, par);
-      } else if (MAPFX_SPLIT_ALT)
-        split_store_wave_alt<WIN, LL, OCC>(g, a, sp, own + par * 64 * RECB, rtab,
-                                           (unsigned char*)(rtab + 256), e0, threadIdx.x & 63, par);
-      else if (MAPFX_SPLIT_WAVES == 2) split_store_wave<WIN, LL, ROLE_ALL, OCC>(g, a, sp, own, e0, threadIdx.x & 63);
-      else if (threadIdx.x < 128) split_store_wave<WIN, LL, ROLE_REC>(g, a, sp, own, e0, threadIdx.x & 63);
-      else split_store_wave<WIN, LL, ROLE_SMALL>(g, a, sp, own, e0, threadIdx.x & 63);
+      const int par = (int)(threadIdx.x >> 6) - 1;            // this wave's step parity
+      // [M1: 64 / LL maps][info: 2 steps][edge: 2 steps][staged records: 2 waves][fold]
+      unsigned char* m1 = lds + g.wv_off_split;
+      unsigned char* inf = m1 + (64 / LL) * g.map_env_bytes;
+      unsigned char* eri = inf + SPLIT_DBM_INFO;
+      unsigned char* ownd = eri + SPLIT_DBM_EDGE;
+      double* rt = (double*)(ownd + 2 * 64 * RECB);
+      split_store_wave_dbm<WIN, LL, OCC>(g, a, lds + g.wv_off_map, m1, inf, eri, ownd + par * 64 * RECB, rt,
+                                         (unsigned char*)(rt + 256), e0, threadIdx.x & 63, par);
       return;
     }
     if (MAPFX_PRIO_STEP) __builtin_amdgcn_s_setprio(MAPFX_PRIO_STEP);
   }
-  // MAPFX_SPLIT_MOVE: wave 1 is the MAP wave (it runs the prologue below with wave 0)
-  const bool is_map = SPLIT && MAPFX_SPLIT_MOVE && threadIdx.x >= 64;
   constexpr int WW = WIN * WIN;
   constexpr int H2 = WIN / 2;
   constexpr int REC = 2 * WW;  // record bytes per agent
@@ -2252,7 +1744,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
   const int pitch = g.pitch;
   const int Wd = g.W;
   const bool want_win = WIN > 0 && (RUNNER || a.obs_window);
-  const int nenv = FULLW ? EPW : min(EPW, g.E - env0);
   const int cell0 = g.P * pitch + g.pl;  // padded index of cell (0, 0)
 
   unsigned char* map = lds + g.wv_off_map + slot * g.map_env_bytes;
@@ -2302,7 +1793,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
   const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared || !env_ok ? 0 : (long long)env * g.map_stride));
   // (the split kernel's three waves build the rows together: lane ag + 16 w of 48)
   constexpr int RPF = SPLIT ? 1 : 4;
-  const int bl = SPLIT ? ag + LL * (int)(threadIdx.x >> 6) : ag, bnl = SPLIT ? LL * MAPFX_SPLIT_WAVES : L;
+  const int bl = ag, bnl = SPLIT ? LL * SPLIT_WAVES : L;
   uint32_t pfw[RPF][3];
   if (g.wv_fast) fast_row_prefetch<RPF>(g, bsrc, bl, bnl, pfw);
   int tcur = env_ok ? a.t[env] : 0;  // (issued first: its pointer is preloaded)
@@ -2328,8 +1819,8 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
   }
   if (!g.wv_fast) wave_fence();
   PSTAMP(1);
-  // MAPFX_SPLIT_DBM: the odd steps' map M1 of this env (at the start of the split region)
-  constexpr bool DBM = SPLIT && MAPFX_SPLIT_DBM && WIN > 0;
+  // the split's second count map M1 (odd steps) of this env, at the start of the split region
+  constexpr bool DBM = SPLIT;
   uint32_t* m1_32 = DBM ? (uint32_t*)(lds + g.wv_off_split + slot * g.map_env_bytes) : nullptr;
   if (g.wv_fast) build_map_rows_fast<MAPFX_FAST_WPR, RPF>(g, map32, bsrc, bl, bnl, pfw, m1_32);
   else build_map_rows_c(g, map32, bitsL, ag, L);
@@ -2340,18 +1831,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
   if constexpr (SPLIT) split_barrier();  // + the store waves' rows
   else wave_fence();
   PSTAMP(2);
-  // MAPFX_SPLIT_MOVE fast mode: no agent of the block stands on an obstacle, nor is
-  // reset onto one (both waves find the same answer from the same agents)
-  bool fast = false;
-  if constexpr (SPLIT && MAPFX_SPLIT_MOVE) {
-    int icell = cur;
-    if (a.autoreset && a.init_pos) {
-      const int2 p = ((const int2*)a.init_pos)[oa];
-      icell = cell0 + p.x * pitch + p.y;
-    }
-    fast = __ballot(((map[cur] | map[icell]) & 0x80u) != 0) == 0;
-  }
-  if (has && !is_map) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
+  if (has) atomicAdd(&map32[cur >> 2], 1u << ((cur & 3) * 8));
   if (DBM && has) atomicAdd(&m1_32[cur >> 2], 1u << ((cur & 3) * 8));
   wave_fence();
 
@@ -2365,7 +1845,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
   auto fold = [&](int buf) {
     const double* rw = rewL + buf * rew_buf + slot * rew_row;
     double R = 0.0;
-    if (MAPFX_ABLATE & 2) return R;
     if constexpr (FIXN) {
 #pragma unroll
       for (int j0 = 0; j0 < LL; j0 += 16) {
@@ -2408,17 +1887,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
       if (do_step && a.reward_f32) a.reward_f32[ei] = (float)R;
       if (do_step && a.err && skip_t) atomicCAS(a.err, 0, env + 1);
     }
-    if (want_win && !MAPFX_DIRECT_REC && !(MAPFX_ABLATE & 4)) {  // staging -> HBM, 16 B/lane
-      const unsigned char* stg = lds + g.wv_off_stage + buf * g.wv_stage_buf;
-      const uint32_t bytes = (uint32_t)(nenv * N * REC);
-      unsigned char* dst = (unsigned char*)a.obs_window + (size_t)(se_t + env0) * N * REC;
-      if ((((uintptr_t)dst) & 15) == 0 && (bytes & 15) == 0) {
-        for (uint32_t i = lane64; i < (bytes >> 4); i += 64)
-          ((uint4*)dst)[i] = ((const uint4*)stg)[i];
-      } else {
-        for (uint32_t i = lane64; i < bytes; i += 64) dst[i] = stg[i];
-      }
-    }
   };
 
   // ---- state of step q = s-1 saved for its heavy part (C) ----
@@ -2451,35 +1919,8 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
     return edge;
   };
 
-  int hslot = 0;  // SPLIT + MAPFX_SPLIT_LAG: ring slot of the next step image
   // HEAVY part of step q (slot qs): window, node, edge, reward, per-agent stores.
   auto heavy = [&](int qs) {
-    if constexpr (SPLIT) {  // step q's info word and raw window rows -> image (qs + 1) & 1
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      using SL = SplitLayout<WIN, LL>;
-      const int edge = edge_of();
-      const int hs = MAPFX_SPLIT_LAG ? hslot : ((qs + 1) & 1);  // LAG: ring slot qs % 3
-      if (MAPFX_SPLIT_LAG) hslot = hslot == SPLIT_NIMG - 1 ? 0 : hslot + 1;
-      u32x4* sl = (u32x4*)__builtin_assume_aligned(
-          lds + g.wv_off_split + hs * g.wv_split_buf + lane64 * SLOT_LANE, 16);
-      const uint32_t fl = (q_dn ? SF_DONE : 0u) | (q_live ? SF_LIVE : 0u) | (q_dnold ? SF_DNOLD : 0u) |
-                          (q_envc ? SF_ENVC : 0u) | (q_skip ? SF_SKIP : 0u) |
-                          (q_alldone ? SF_ALLDONE : 0u) | ((uint32_t)(edge > 255 ? 255 : edge) << 8);
-      uint32_t w[SL::SLOT / 4];
-      w[0] = (uint32_t)q_nc;
-      w[1] = q_nb;
-      w[2] = fl;
-      w[3] = (uint32_t)q_tcur;
-#pragma unroll
-      for (int i = 0; i < SL::NXW; ++i) w[4 + i] = qx[i];
-#pragma unroll
-      for (int i = 4 + SL::NXW; i < SL::SLOT / 4; ++i) w[i] = 0;
-#pragma unroll
-      for (int i = 0; i < SL::SLOT / 16; ++i)  // chunk-major: lanes write consecutive 16-B chunks
-        if (!(MAPFX_ABLATE & 2048) || i == 0)   // (diagnostic 2048: the info chunk only)
-          sl[SLOT_CHUNK * i] = u32x4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
-      return;
-    }
     const uint32_t so = ROLL ? (uint32_t)qs * EN : 0u;
     const int buf = ROLL ? (qs & 1) : 0;
     uint32_t node = 0;
@@ -2498,29 +1939,14 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
     const uint32_t nzn = (((q_nb & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) >> 7) & 0x01010101u;
     const uint32_t availm = __builtin_amdgcn_udot4(nzn, 0x08040201u, 16u, false);
     if constexpr (WIN > 0) {
-      if (want_win && has && !(MAPFX_ABLATE & 1)) {
-#if MAPFX_DIRECT_REC
-#ifdef MAPFX_DIAG_COAL  // diagnostic only: same record words, lane-contiguous 16 B stores
-        {
-          constexpr int NW = (REC + 3) / 4;
-          uint32_t w[NW];
-          rec_words<WIN>(R, w, std::make_integer_sequence<int, NW>{});
-          uint4* d = (uint4*)((unsigned char*)a.obs_window + (size_t)(so + env0 * N) * REC) + lane64 * 3;
-          d[0] = make_uint4(w[0], w[1], w[2], w[3]);
-          d[1] = make_uint4(w[4], w[5], w[6], w[7]);
-          d[2] = make_uint4(w[8], w[9], w[10], w[11] ^ w[12]);
-        }
-#else
+      if (want_win && has) {
+        // the record straight to HBM from registers (records staged in LDS for 16-byte
+        // stores measured slower for the per-step launch)
         write_record<WIN>(R, a.obs_window, (so + oa) * (uint32_t)REC);
-#endif
-#else
-        stage_record<WIN>(R, lds + g.wv_off_stage + buf * g.wv_stage_buf +
-                                 (uint32_t)(slot * N + ag) * REC);  // -> LDS staging
-#endif
       }
     }
     const uint32_t ai = so + oa;
-    if (has && !(MAPFX_ABLATE & 8)) {
+    if (has) {
       const int2 rc = cell_rc(q_nc);
       if (RUNNER) {
         a.node[ai] = (uint8_t)node;
@@ -2547,7 +1973,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
     }
     if (do_step && (FIXN || ag < rew_row))  // lanes past N pad the row with +0.0
       rewL[buf * rew_buf + slot * rew_row + ag] = has ? rr : 0.0;
-    if (has && !(MAPFX_ABLATE & 8)) {
+    if (has) {
       if (RUNNER || (do_step && a.edge)) a.edge[ai] = (uint8_t)(edge > 255 ? 255 : edge);
     }
   };
@@ -2601,124 +2027,8 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
     return act_;
   };
 
-  if constexpr (SPLIT && MAPFX_SPLIT_MOVE && WIN > 0) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    constexpr int RECB = OCC ? WIN * WIN : 2 * WIN * WIN;
-    u32x4* ring = (u32x4*)__builtin_assume_aligned(
-        lds + g.wv_off_split + SPLIT_NIMG * g.wv_split_buf + 2 * 64 * RECB + SPLIT_FOLD_LDS, 16);
-    if (is_map) {
-      if (!fast) {  // the one-wave step side runs on wave 0: only its barriers
-        for (int s = 1; s <= T + 1; ++s) split_barrier();
-        return;
-      }
-      // ---- MAP wave: step q of the MOVE wave's ring -> agent-count map, dep map,
-      // edge test (:364-383), window rows, the step image for the store waves ----
-      int mcur = cur;  // where this lane's agent stands in the count map
-      for (int s = 1; s <= T + 1; ++s) {
-        split_barrier();  // step s - 1's ring record is published
-        if (s > T) break;
-        const int q = s - 1;
-        const u32x4 r = ring[(q & 1) * 64 + lane64];
-        const int oc = (int)(r.x & 0xFFFFu), nc = (int)(r.x >> 16);
-        const uint32_t f = r.y;
-        if (__ballot(oc != mcur)) {  // the env was reset after step q - 1 (autoreset)
-          if (oc != mcur) {
-            atomicSub(&map32[mcur >> 2], 1u << ((mcur & 3) * 8));
-            atomicAdd(&map32[oc >> 2], 1u << ((oc & 3) * 8));
-          }
-        }
-        const uint32_t v = map[nc];  // the target's pre-step byte (moved lanes)
-        const bool mvd = (f & 128u) != 0;
-        const int act = (int)((f >> 8) & 0xFFu);
-        dep[oc] = (unsigned char)(mvd ? (uint32_t)act : 0x7Fu);
-        atomicAdd(&map32[oc >> 2], mvd ? 0u - (1u << ((oc & 3) * 8)) : 0u);
-        atomicAdd(&map32[nc >> 2], mvd ? 1u << ((nc & 3) * 8) : 0u);
-        uint32_t x[3 * NX];
-        {
-          const int w0 = (nc - H2 * pitch - H2) >> 2;
-          const int wpr = pitch >> 2;
-#pragma unroll
-          for (int y = 0; y < WIN; ++y) {
-            x[y] = map32[w0 + y * wpr];
-            x[WIN + y] = map32[w0 + y * wpr + 1];
-            x[2 * WIN + y] = WIN > 5 ? map32[w0 + y * wpr + 2] : 0u;
-          }
-        }
-        const uint32_t dj = dep[nc];
-        const int o8 = ((nc - H2) & 3) * 8;
-        const auto row64 = [&](int y) { return ((uint64_t)x[WIN + y] << 32) | x[y]; };
-        const uint32_t up = (uint32_t)(row64(H2 - 1) >> (o8 + 8 * H2)) & 0xFFu;
-        const uint32_t dw = (uint32_t)(row64(H2 + 1) >> (o8 + 8 * H2)) & 0xFFu;
-        const uint32_t cr = (uint32_t)(row64(H2) >> (o8 + 8 * (H2 - 1)));
-#pragma unroll
-        for (int i = 0; i < 3 * NX; ++i) qx[i] = x[i];
-        q_oc = oc;
-        q_nc = nc;
-        q_act = act;
-        q_pre = (int)(v & 0x7Fu) - 1 + (int)(v >> 7);
-        q_dj = dj;
-        q_nb = up | (dw << 8) | ((cr & 0xFFu) << 16) | (((cr >> 16) & 0xFFu) << 24);
-        q_moved = mvd;
-        q_envc = (f & SF_ENVC) != 0;
-        q_dnold = (f & SF_DNOLD) != 0;
-        q_dn = (f & SF_DONE) != 0;
-        q_live = (f & SF_LIVE) != 0;
-        q_skip = (f & SF_SKIP) != 0;
-        q_alldone = (f & SF_ALLDONE) != 0;
-        q_tcur = (int)r.z;
-        heavy(q);  // image (q + 1) & 1, published by the next barrier
-        mcur = nc;
-      }
-      return;
-    }
-    if (fast) {
-      // ---- MOVE wave: the dynamics (:85-141) from the static obstacle flags (bit 7
-      // of the count map, never touched by the MAP wave's count updates) ----
-      for (int s = 0; s < T; ++s) {
-        const int act = next_action(s);
-        const int oc = cur;
-        const bool mv = !dn && (uint32_t)act < 4u;
-        const bool obst = mv && ((nb >> ((act & 3) * 8)) & 0x80u) != 0;  // obstacle / border
-        const bool envc = obst;
-        const bool skip = (__ballot(act == 0xFF) & envmask) != 0;
-        const bool moved = mv && !obst && !skip;
-        int dlt = (act & 2) ? 1 : pitch;  // 0: up, 1: down, 2: left, 3: right
-        dlt = (act & 1) ? dlt : -dlt;
-        const int nc = moved ? oc + dlt : oc;
-        const bool dn_old = dn;
-        const bool live = !skip;
-        if (live && nc == gcell) dn = true;          // :112-114
-        if (live && tcur + 1 >= g.limit) dn = true;  // :116-117
-        if (live && !dn_old) ++st;
-        if (!skip) ++tcur;
-        const bool alldone = (__ballot(!dn) & envmask) == 0;
-        const uint32_t f = (dn ? SF_DONE : 0u) | (live ? SF_LIVE : 0u) | (dn_old ? SF_DNOLD : 0u) |
-                           (envc ? SF_ENVC : 0u) | (skip ? SF_SKIP : 0u) | (alldone ? SF_ALLDONE : 0u) |
-                           (moved ? 128u : 0u) | ((uint32_t)act << 8);
-        ring[(s & 1) * 64 + lane64] = u32x4{(uint32_t)oc | ((uint32_t)nc << 16), f, (uint32_t)tcur, 0u};
-        cur = nc;
-        if (a.autoreset && alldone) {  // the MAP wave moves the counts when it sees oc != its cell
-          const int2 p = ((const int2*)a.init_pos)[oa];
-          cur = cell0 + p.x * pitch + p.y;
-          dn = false;
-          st = 0;
-          tcur = 0;
-        }
-        nb = (uint32_t)map[cur - pitch] | ((uint32_t)map[cur + pitch] << 8) |
-             ((uint32_t)map[cur - 1] << 16) | ((uint32_t)map[cur + 1] << 24);
-        split_barrier();  // ring slot s & 1 -> MAP wave
-      }
-      split_barrier();  // the MAP wave's last image
-      ((int2*)a.pos)[oa] = cell_rc(cur);
-      a.done[oa] = dn ? 1 : 0;
-      if (a.steps) a.steps[oa] = st;
-      if (ag == 0) a.t[env] = tcur;
-      return;
-    }
-  }
-
   if constexpr (DBM) {
-    // ---- MAPFX_SPLIT_DBM step wave: map s & 1 is moved from the positions after step
+    // ---- the split's step wave: map s & 1 is moved from the positions after step
     // s - 2 to those after step s; the store waves read step s's window rows from it ----
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     unsigned char* m1 = (unsigned char*)m1_32;
@@ -2835,8 +2145,8 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
     int dlt = (act & 2) ? 1 : pitch;  // 0: up, 1: down, 2: left, 3: right
     dlt = (act & 1) ? dlt : -dlt;
     const int nc = moved ? oc + dlt : oc;
-    if (has && !(MAPFX_ABLATE & 64)) dep[oc] = (unsigned char)(moved ? (uint32_t)act : 0x7Fu);
-    if (!(MAPFX_ABLATE & 16)) {
+    if (has) dep[oc] = (unsigned char)(moved ? (uint32_t)act : 0x7Fu);
+    {
 #ifndef MAPFX_FULLW_ATOMICS
 #define MAPFX_FULLW_ATOMICS 1
 #endif
@@ -2857,32 +2167,26 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
       const int wpr = pitch >> 2;
 #pragma unroll
       for (int y = 0; y < WIN; ++y) {
-        if ((MAPFX_ABLATE & 131072) && (y < H2 - 1 || y > H2 + 1)) {  // diagnostic: the 3 middle rows
-          x[y] = x[WIN + y] = x[2 * WIN + y] = 0x01010101u;
-          continue;
-        }
         x[y] = map32[w0 + y * wpr];
         x[WIN + y] = map32[w0 + y * wpr + 1];
         x[2 * WIN + y] = WIN > 5 ? map32[w0 + y * wpr + 2] : 0u;
       }
-    } else if (!(MAPFX_ABLATE & 32)) {
+    } else {
       x[0] = map[nc];  // centre (node), then up / down / left / right
       x[1] = map[nc - pitch];
       x[2] = map[nc + pitch];
-    } else {
-      x[0] = x[1] = x[2] = 1u;
     }
     uint32_t xl = 0, xr = 0;
     if constexpr (WIN == 0) {
       xl = map[nc - 1];
       xr = map[nc + 1];
     }
-    const uint32_t dj = (MAPFX_ABLATE & 64) ? 0xFFu : dep[nc];  // pre-step occupant's move
-    const double Rp = (!SPLIT && ROLL && do_step) ? fold(s & 1) : 0.0;  // step s-2's row
+    const uint32_t dj = dep[nc];  // pre-step occupant's move
+    const double Rp = (ROLL && do_step) ? fold(s & 1) : 0.0;  // step s-2's row
     STAMP(1);
     // ---------------- C: heavy part of step s-1, env outputs of step s-2 -----------
     if (s > 0) heavy(s - 1);
-    if (!SPLIT && ROLL && s > 1) tail(s & 1, p_se, p_skip, p_alldone, p_tcur, Rp);
+    if (ROLL && s > 1) tail(s & 1, p_se, p_skip, p_alldone, p_tcur, Rp);
     STAMP(3);
     // ---------------- D: step s's neighbours, dones, t (:112-117) ----------------
     uint32_t nbn;
@@ -2898,7 +2202,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
       nbn = (x[1] & 0xFFu) | ((x[2] & 0xFFu) << 8) | ((xl & 0xFFu) << 16) | ((xr & 0xFFu) << 24);
     }
     const bool dn_old = dn;
-    const bool live = !skip && !(MAPFX_ABLATE & 128);
+    const bool live = !skip;
     if (live && nc == gcell) dn = true;          // :112-114 (goal reached)
     if (live && tcur + 1 >= g.limit) dn = true;  // :116-117 (t is incremented below)
     if (live && !dn_old) ++st;
@@ -2965,12 +2269,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
       }
     }
     STAMP(4);
-    if constexpr (SPLIT) {  // image s & 1 (LAG: the previous iteration's image) -> store waves
-      if constexpr (MAPFX_SPLIT_LAG && WIN > 0) split_barrier_lag<SplitLayout<WIN, LL>::SLOT / 16>();
-      else split_barrier();
-    } else {
-      wave_fence();
-    }
+    wave_fence();
     STAMP(6);
   }
 #ifdef MAPFX_CLOCKS
@@ -2987,11 +2286,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * MAPFX_SPLIT_WAVES : 64, SPLIT ? M
   }
 #endif
   // ---- drain the pipeline: heavy part of the last step, the last two tails ----
-  if (SPLIT && T > 0) {
-    heavy(T - 1);
-    if constexpr (SPLIT && MAPFX_SPLIT_LAG && WIN > 0) split_barrier_lag<SplitLayout<WIN, LL>::SLOT / 16>();
-    split_barrier();  // image T & 1 (LAG: ring slot (T - 1) % 3): the last step
-  } else if (T > 0) {
+  if (T > 0) {
     const double Rp = (ROLL && T > 1) ? fold(T & 1) : 0.0;  // step T-2's row
     heavy(T - 1);
     if (ROLL && T > 1) tail(T & 1, p_se, p_skip, p_alldone, p_tcur, Rp);
@@ -3138,7 +2433,7 @@ int check_hip(hipError_t e, const char* what) {
 template <int WIN>
 KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split, bool occ, bool short_t) {
   if (occ) {  // obs_window_occ: only the store-wave split writes it on the wave path
-    if constexpr (WIN > 0 && (MAPFX_SPLIT_ALT || MAPFX_SPLIT_WAVES == 2)) {
+    if constexpr (WIN > 0) {
       if (roll && runner && split && fullw && L == 16)
         return short_t ? mapf_wave_kernel<WIN, true, true, true, 16, true, true, 8>
                        : mapf_wave_kernel<WIN, true, true, true, 16, true, true>;
@@ -3189,22 +2484,17 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
     const uintptr_t al16 = (uintptr_t)a.obs_window | (uintptr_t)a.obs_window_occ | (uintptr_t)a.traj_pos |
                            (uintptr_t)a.node | (uintptr_t)a.edge | (uintptr_t)a.avail |
                            (uintptr_t)a.traj_done | (uintptr_t)a.reward | (uintptr_t)a.traj_t;
-    // + staged-record images of the store wave (2 x 64 records)
-    // (+ ALT: the 256-entry reward table and the 32-step code ring)
-    const int split_lds =
-        MAPFX_SPLIT_DBM
-            // M1 (the odd steps' maps of the wave's envs), info + edge rings, staged records, fold
-            ? g.wv_lds + g.EPW * g.map_env_bytes + SPLIT_DBM_INFO + SPLIT_DBM_EDGE +
-                  2 * 64 * (occ ? g.wlen / 2 : g.wlen) + SPLIT_FOLD_LDS
-            : g.wv_lds + SPLIT_NIMG * g.wv_split_buf + 2 * 64 * (occ ? g.wlen / 2 : g.wlen) +
-                  (MAPFX_SPLIT_ALT ? SPLIT_FOLD_LDS : 0) + (MAPFX_SPLIT_MOVE ? SPLIT_RING_LDS : 0);
-    const bool split = MAPFX_SPLIT && runner && fullw && g.L == 16 && g.wv_split_buf > 0 &&
+    // the split's LDS: M1 (the odd steps' maps of the wave's envs), info + edge rings, the
+    // two store waves' staged records, the reward-code table and ring
+    const int split_lds = g.wv_lds + g.EPW * g.map_env_bytes + SPLIT_DBM_INFO + SPLIT_DBM_EDGE +
+                          2 * 64 * (occ ? g.wlen / 2 : g.wlen) + SPLIT_FOLD_LDS;
+    const bool split = MAPFX_SPLIT && runner && fullw && g.L == 16 && g.wv_split_ok &&
                        split_lds <= 64 * 1024 && (al16 & 15) == 0;
     KernelFn fn = pick_wave_kernel((a.obs_window || occ) ? g.window : 0, roll, fullw, runner, g.L, split, occ,
                                    roll && a.T <= MAPFX_AB_SHORT_T);
     if (fn) {
       const int blocks = (g.E + g.EPW - 1) / g.EPW;
-      const dim3 bt(split ? 64 * MAPFX_SPLIT_WAVES : 64);
+      const dim3 bt(split ? 64 * SPLIT_WAVES : 64);
       const unsigned ldsb = split ? split_lds : g.wv_lds;
       if (ev0 || ev1)
         hipExtLaunchKernelGGL(fn, dim3(blocks), bt, ldsb, stream, ev0, ev1, 0, MAPFX_HOT_ARGS(a, g, blocks), a, g);
@@ -3422,7 +2712,6 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   g.limit = c.episode_limit;
   g.step_rew = c.step_reward;
   g.collide_rew = c.collide_reward;
-  g.stage_env_bytes = (c.obs_mode & MAPFX_OBS_WINDOW) ? N * g.wlen * es : 0;  // wave kernels' staging
   g.m_N = magic48(N);
   g.m_w = magic48(std::max(1, c.window));
   g.m_ww = magic48(std::max(1, c.window * c.window));
@@ -3512,15 +2801,10 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     g.wv_rew_buf = round_up(EPW * g.wv_rew_row * 8, 16);
     g.wv_off_rew = o;
     o += 2 * g.wv_rew_buf;
-    g.wv_stage_buf = MAPFX_DIRECT_REC ? 0 : round_up(EPW * g.stage_env_bytes, 16);
-    g.wv_off_stage = o;
-    o += 2 * g.wv_stage_buf;
     g.wv_lds = o;
-    // store-wave split images (placed after the wave layout; only that kernel allocates them)
+    // the store-wave split's LDS (after the wave layout; only that kernel allocates it)
     g.wv_off_split = o;
-    g.wv_split_buf = L != 16 ? 0 : c.window == 3 ? SplitLayout<3, 16>::BYTES
-                                 : c.window == 5 ? SplitLayout<5, 16>::BYTES
-                                 : c.window == 7 ? SplitLayout<7, 16>::BYTES : 0;
+    g.wv_split_ok = (L == 16 && (c.window == 3 || c.window == 5 || c.window == 7)) ? 1 : 0;
     g.wave_ok = (o <= 64 * 1024 && pitch < 256 && g.rows * pitch < 65536) ? 1 : 0;
   }
 

@@ -37,18 +37,6 @@
 #include "mapfx.h"
 #include "mapfx_partial.h"
 
-#ifndef PARTIAL_EARLY_WB
-#define PARTIAL_EARLY_WB 1  // partial_kernel: state / avail / post rows stored right after the step
-#endif
-#ifndef PARTIAL_STAGE_FIRST
-// 1: partial_kernel stages the bitmap before issuing the state loads (its wait then covers
-// one load, not all; the map build overlaps the rest).  Measured round 4: 15.73 vs
-// 15.42 us per step (gpurun_out/r04u) -- slower, so off.
-#define PARTIAL_STAGE_FIRST 0
-#endif
-#ifndef PABL
-#define PABL 0  // diagnostic builds only: 1 skip the obs rows, 2 skip the step, 4 skip the staged copy
-#endif
 
 #ifdef PARTIAL_STAMPS
 // Diagnostic build only (never the shipped library): s_memtime stamps of partial_kernel's
@@ -955,15 +943,6 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   const bool nb_carry = a.pnbr && a.pdist && !g.gd32;  // neighbour distances carried
   const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)ec_ * g.map_stride));
   const uint32_t bw0 = bsrc[ag < g.bits_words ? ag : 0];  // this lane's first bitmap word
-#if PARTIAL_STAGE_FIRST
-  // the bitmap staged before the state loads are issued: the wait is for this one load
-  // (after the state loads the compiler's wait covered all of them), and the map build
-  // then overlaps their latency
-  if (env_ok) {
-    if (ag < g.bits_words) bitsL[ag] = bw0;
-    for (int w = ag + g.L; w < g.bits_words; w += g.L) bitsL[w] = bsrc[w];  // maps past 16 x 32 words
-  }
-#endif
   // the step's action: one 8-byte load of the aligned block that holds it (whatever the
   // dtype: the block lies in the element's page), decoded after the map build; the
   // runner's address needs the env's row of the MAC output first
@@ -999,12 +978,12 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
     epl_raw = a.ra.ep_length[ec_];
   }
   // ---- LDS map (c format) + dep map (obstacle flag in bit 7) ----
-#if !PARTIAL_STAGE_FIRST
+  // (staging the bitmap before the state loads are issued measured slower: 15.73 vs
+  // 15.42 us per step)
   if (env_ok) {
     if (ag < g.bits_words) bitsL[ag] = bw0;
     for (int w = ag + g.L; w < g.bits_words; w += g.L) bitsL[w] = bsrc[w];  // maps past 16 x 32 words
   }
-#endif
   PST(1);
   wave_fence();
   if (env_ok) {
@@ -1107,7 +1086,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
 
   // ---- step (:165-310) ----
   double Rsum = 0.0;  // sum(rewards) of the env (agent-0 lane)
-  if (a.do_step && env_ok && !(PABL & 2)) {
+  if (a.do_step && env_ok) {
     const bool skip = (__ballot(act < 0) & envmask) != 0;  // the reference asserts (:174)
     if (!skip) {
       ++tcur;  // :178
@@ -1226,7 +1205,6 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   const int nbd2 = gt[c > 0 ? -1 : 0], nbd3 = gt[c + 1 < g.W ? 1 : 0];
 
   PST(8);
-#if PARTIAL_EARLY_WB
   // ---- the step's results leave before the observation rows are built: their stores
   // then queue ahead of the rows' copy-out instead of behind it ----
   // avail (:399-433): neighbour in bounds and not a free-standing obstacle
@@ -1299,7 +1277,6 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
     }
     if (ag == 0) ra.alive_prev[env] = live0;
   }
-#endif
   // ---- observations of the current state (:312-391) ----
   // per-agent feature rows: curr, start, goal, unit vec, norm, node, edge, steps
   if (has) {
@@ -1328,7 +1305,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   // the K-nearest rows are built, measured 19.0 vs 15.2 us: chunks of partial lines.)
   constexpr bool FAST = KF > 0 && LF > 0;
   const bool one_run = a.obs_rows == nullptr;
-  const bool staged = FAST && (a.obs || a.obs_rows) && g.off_stage >= 0 && !(PABL & 4);
+  const bool staged = FAST && (a.obs || a.obs_rows) && g.off_stage >= 0;
   // this lane's row of group gi's image (G lanes per group)
   auto stage_row = [&](int gi, int G, int i0, int i1) {
     const int s0 = (G * gi) >> g.lshift;
@@ -1389,7 +1366,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
         ((uint32_t*)(gdst + head + body))[lane64] = ((const uint32_t*)(img + head + body))[lane64];
     }
   };
-  if (has && my_obs && !(PABL & 1)) {
+  if (has && my_obs) {
     if constexpr (FAST) {
       // -------- fast path: the whole row in registers --------
       if constexpr (WIN > 0) {  // window planes (:327-342) from whole map words
@@ -1503,7 +1480,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
                          ((uint32_t)nbd2 & 0xFFFFu) | ((uint32_t)nbd3 << 16));
   asm volatile("" : "+v"(nb1.x), "+v"(nb1.y));
   if constexpr (FAST) {
-    if (g.off_stage < 0 && has && my_obs && !(PABL & 1)) {  // rows straight to HBM (per-lane stores)
+    if (g.off_stage < 0 && has && my_obs) {  // rows straight to HBM (per-lane stores)
       uint32_t* d = (uint32_t*)(my_obs + ag * DF);
 #pragma unroll
       for (int i = 0; i < DF; ++i) d[i] = __float_as_uint(o[i]);
@@ -1524,78 +1501,6 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   }
   PST(11);
   (void)o;
-#if !PARTIAL_EARLY_WB
-  // avail (:399-433): neighbour in bounds and not a free-standing obstacle
-  uint32_t am = 16u;
-  if (has && (a.avail || a.ra.ep_avail)) {
-    if (map[cur - pitch]) am |= 1u;
-    if (map[cur + pitch]) am |= 2u;
-    if (map[cur - 1]) am |= 4u;
-    if (map[cur + 1]) am |= 8u;
-    if (a.avail) a.avail[oa] = (uint8_t)am;
-  }
-  // state (:377-387): [total collisions, step count, sum(each goal cost)]
-  const int gsum = group_sum(has ? gcost : 0, g.L);
-  if (env_ok && ag == 0 && a.state) {
-    a.state[3 * env + 0] = (float)total;
-    a.state[3 * env + 1] = (float)tcur;
-    a.state[3 * env + 2] = (float)gsum;
-  }
-  // ---- state write-back ----
-  if (has) {
-    ((int2*)a.pos)[oa] = make_int2(r, c);
-    a.steps[oa] = steps;
-    a.at_goal[oa] = at_goal ? 1 : 0;
-    a.done[oa] = dn ? 1 : 0;
-    a.goal_cost[oa] = gcost;
-    a.node[oa] = (uint8_t)node;
-    a.edge[oa] = edge;
-    if (a.pdist) a.pdist[oa] = pd;
-    if (runner && arow >= 0) {  // the EpisodeBatch's actions / actions_onehot rows at ts
-      const long long v = act_value(alo, ahi);
-      if (a.ra.ep_actions)
-        a.ra.ep_actions[(long long)env * a.ra.ep_actions_sb + (long long)a.ra.ts * a.ra.ep_actions_st + ag] = v;
-      if (a.ra.ep_onehot) {
-        float* oh = a.ra.ep_onehot + (long long)env * a.ra.ep_onehot_sb +
-                    (long long)a.ra.ts * a.ra.ep_onehot_st + (long long)ag * 5;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) oh[k] = v == k ? 1.0f : 0.0f;
-      }
-    }
-  }
-  if (env_ok && ag == 0) {
-    a.t[env] = tcur;
-    a.terminated[env] = term ? 1 : 0;
-    a.total_coll[env] = total;
-  }
-  if (post && env_ok) {  // runner_post_kernel (runner.hip) for a running env, fused
-    const mapfx_runner_acts& ra = a.ra;
-    if (live0) {
-      if (ag == 0) {
-        if (ra.ep_reward) ra.ep_reward[(long long)env * ra.ep_reward_sb + (long long)ra.ts * ra.ep_reward_st] = (float)Rsum;
-        // env_terminated = terminated and not info.get("episode_limit") (parallel_runner.py:146-150):
-        // MARL_PARTIAL's info has no "episode_limit" key
-        if (ra.ep_term) ra.ep_term[(long long)env * ra.ep_term_sb + (long long)ra.ts * ra.ep_term_st] = term ? 1 : 0;
-        ra.ep_return[env] = epr0 + Rsum;
-        ra.ep_length[env] = epl0 + 1;
-        ra.alive[env] = term ? 0 : 1;
-        if (ra.ep_state) {  // update(pre_transition_data, bs, ts + 1): state, avail, filled
-          float* d = ra.ep_state + (long long)env * ra.ep_state_sb;
-          d[0] = (float)total;
-          d[1] = (float)tcur;
-          d[2] = (float)gsum;
-        }
-        if (ra.ep_filled) ra.ep_filled[(long long)env * ra.ep_filled_sb] = 1;
-      }
-      if (has && ra.ep_avail) {
-        int32_t* d = ra.ep_avail + (long long)env * ra.ep_avail_sb + ag * 5;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) d[k] = (int32_t)((am >> k) & 1u);
-      }
-    }
-    if (ag == 0) ra.alive_prev[env] = live0;
-  }
-#endif
   // the carried neighbour distances are stored last (their loads land during the rows)
   if (has && nb_carry) ((uint2*)a.pnbr)[oa] = nb1;
   PST(12);

@@ -585,13 +585,14 @@ def profile_traffic(leg, kernel=None, path=None, **match):
     return pm["traffic_bytes_per_launch"], "%s: %s" % (rel, pm.get("command", "rocprofv3 --pmc passes"))
 
 
-def partial_bytes_per_env_step(N, D, HW):
+def partial_bytes_per_env_step(N, D, HW, gd_bytes=2):
     """Algorithmic HBM bytes of one MARL_PARTIAL env step (state round-trips HBM):
     reads actions N + state 27N + 13 (pos 8, steps 4, at_goal 1, done 1, goal_cost 4,
-    node 1, edge 4, carried goal distance 4 per agent) + goal/init 16N + one 2-byte
-    goal-distance read per (moving) agent 2N + bitmap HW/8; writes obs 4DN + reward 8
-    + state 12 + avail N + state 27N + 9."""
-    return (N + 27 * N + 13 + 16 * N + 2 * N + HW // 8) + (4 * D * N + 8 + 12 + N + 27 * N + 9)
+    node 1, edge 4, carried goal distance 4 per agent) + goal/init 16N + one goal-distance
+    entry per (moving) agent (gd_bytes: 1 for the u8 tables of maps up to 255 cells, 2
+    for int16) + bitmap HW/8; writes obs 4DN + reward 8 + state 12 + avail N + state
+    27N + 9."""
+    return (N + 27 * N + 13 + 16 * N + gd_bytes * N + HW // 8) + (4 * D * N + 8 + 12 + N + 27 * N + 9)
 
 
 def run_partial(args, dist, rank, world, local):
@@ -671,7 +672,7 @@ def run_partial(args, dist, rank, world, local):
     from mapfx import _abi
     kernel_name = _abi.last_kernel()     # the step instance the graph replays
     D = b.obs_dim
-    bpes = partial_bytes_per_env_step(N, D, S * S)
+    bpes = partial_bytes_per_env_step(N, D, S * S, b.goal_dist.element_size())
     achieved = E * bpes / (kern_ms * 1e-3) / 1e9
     # traffic per launch (one env step of E envs) from the PMC profile of this workload
     traffic, traffic_src = profile_traffic("partial", kernel=kernel_name, E=E, N=N, S=S)
@@ -903,7 +904,7 @@ def run_runner(args, dist, rank, world, local):
     # terminated u8, filled i64) and the MAC's read of the avail row
     D = info["obs_shape"]
     row_bytes = 4 * N * D + 4 * 3 + 4 * 5 * N + 8 * N + 4 * 5 * N + 4 + 1 + 8 + 4 * 5 * N
-    bpes = partial_bytes_per_env_step(N, D, S * S) + row_bytes
+    bpes = partial_bytes_per_env_step(N, D, S * S, runner.env.goal_dist.element_size()) + row_bytes
     achieved = steps * world * bpes / elapsed / 1e9
     if rank == 0:
         print(json.dumps({

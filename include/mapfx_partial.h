@@ -74,8 +74,9 @@ typedef struct mapfx_partial_state {
   const uint8_t* map_bits;  /* [E or 1][mapfx_map_stride(H, W)]                     */
   void* goal_dist;          /* [E][N][H*W] shortest-path lengths to each goal (-1:
                                obstacle / unreachable), filled by
-                               mapfx_partial_goal_dist; int16, or int32 when H*W >
-                               32767 (mapfx_partial_goal_dist_elem_size)            */
+                               mapfx_partial_goal_dist; u8 when H*W <= 255 (255
+                               stands for -1; ABI 5), int16 up to 32767 cells, else
+                               int32 (mapfx_partial_goal_dist_elem_size)            */
   int32_t* pdist;           /* [E][N] goal_dist of each agent's current cell, carried
                                from step to step (the reference's _new_pdist / next
                                _old_pdist, :227-233): a step reads it as opd and looks
@@ -88,7 +89,7 @@ typedef struct mapfx_partial_state {
                                launch: a step
                                takes a moving agent's npd from it instead of a
                                dependent table lookup.  Used only with pdist and
-                               int16 tables (H*W <= 32767); NULL: looked up.
+                               u8 / int16 tables (H*W <= 32767); NULL: looked up.
                                Appended in ABI 4.                                  */
 } mapfx_partial_state;
 
@@ -107,7 +108,8 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out_han
 void mapfx_partial_destroy(mapfx_partial_t* h);
 /* 2*W*W + 13*K (:377 get_obs_size) */
 int32_t mapfx_partial_obs_dim(const mapfx_partial_t* h);
-/* 2 or 4: bytes per goal_dist entry (a path on H*W cells is shorter than H*W). */
+/* 1, 2 or 4: bytes per goal_dist entry (a path on H*W cells is shorter than H*W; the
+ * u8 form (ABI 5) holds -1 as 255). */
 int32_t mapfx_partial_goal_dist_elem_size(int32_t H, int32_t W);
 
 /* BFS distance tables of every (masked) env's goals (:906-928: A* lengths on

@@ -114,7 +114,8 @@ struct PGeo {
   int win, K, D, limit, hw;          // window, knn, obs dim, episode limit, H*W
   double move_rew, stay_rew, stay_goal_rew, nc_rew, ec_rew, env_rew;
   int sq_max, bonus_len;             // LUT sizes
-  int gd32;                          // goal-distance tables are int32 (H * W > 32767), else int16
+  int gd32;                          // goal-distance tables are int32 (H * W > 32767)
+  int gd8;                           // ... u8 (H * W <= 255: 255 = -1), else int16
   int big;                           // workgroup-per-env path (N > 64 or H, W > 256), map in HBM
   int hs_log, wg_lds, huge_lds;      // its LDS hash size (log2), block LDS; huge-map BFS LDS
   uint32_t m_wpr;                    // ceil(2^32 / wpr): wi / wpr = umulhi(wi, m_wpr) below rows * wpr
@@ -135,7 +136,7 @@ struct PArgs {
   uint8_t* terminated;
   int32_t* total_coll;
   const uint8_t* bits;
-  const void* gd;  // int16 or int32 (g.gd32)
+  const void* gd;  // u8, int16 or int32 (g.gd8, g.gd32)
   int32_t* pdist;  // [E][N] goal distance of the current cell (carried), or NULL
   int16_t* pnbr;   // [E][N][4] goal distances of its 4 neighbours (carried with pdist), or NULL
   const void* actions;
@@ -289,11 +290,18 @@ __device__ __forceinline__ int nbr_dist(uint2 nb, int act) {
   return (int)(int16_t)(uint16_t)((act & 1) ? (w >> 16) : (w & 0xFFFFu));
 }
 
-// goal distance of cell `cell` in agent `oa`'s table (int16, or int32 when H * W > 32767:
-// a path can be longer than 32767 cells there)
-__device__ __forceinline__ int goal_dist_at(const PGeo& g, const void* gd, long long oa, int cell) {
-  const long long i = oa * g.hw + cell;
+// entry i of a goal table: u8 while H * W <= 255 (a path is shorter than H * W cells;
+// 255 stands for -1, obstacle / unreachable), int16 up to 32767 cells, else int32
+__device__ __forceinline__ int gd_entry(const PGeo& g, const void* gd, long long i) {
+  if (g.gd8) {
+    const int v = ((const uint8_t*)gd)[i];
+    return v == 255 ? -1 : v;
+  }
   return g.gd32 ? ((const int32_t*)gd)[i] : (int)((const int16_t*)gd)[i];
+}
+// goal distance of cell `cell` in agent `oa`'s table
+__device__ __forceinline__ int goal_dist_at(const PGeo& g, const void* gd, long long oa, int cell) {
+  return gd_entry(g, gd, oa * g.hw + cell);
 }
 
 // The step's goal-path distances (:227-233) with the current cell's distance carried in
@@ -1200,9 +1208,11 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   // here, consumed before the staged copy-out (the observation rows hide their latency)
   // -- unconditional loads (idle lanes read agent 0's table at (0, 0), an off-grid
   // neighbour the cell itself; no branch, so no use of a value can move up to its load)
-  const int16_t* gt = (const int16_t*)a.gd + oc_ * g.hw + r * g.W + c;
-  const int nbd0 = gt[r > 0 ? -g.W : 0], nbd1 = gt[r + 1 < g.H ? g.W : 0];
-  const int nbd2 = gt[c > 0 ? -1 : 0], nbd3 = gt[c + 1 < g.W ? 1 : 0];
+  // (u8 tables, H * W <= 255: the 4 lookups of an agent fall in one 64-byte table, so one
+  // memory request; int16 tables span two)
+  const long long gi = oc_ * g.hw + r * g.W + c;
+  const int nbd0 = gd_entry(g, a.gd, gi + (r > 0 ? -g.W : 0)), nbd1 = gd_entry(g, a.gd, gi + (r + 1 < g.H ? g.W : 0));
+  const int nbd2 = gd_entry(g, a.gd, gi + (c > 0 ? -1 : 0)), nbd3 = gd_entry(g, a.gd, gi + (c + 1 < g.W ? 1 : 0));
 
   PST(8);
   // ---- the step's results leave before the observation rows are built: their stores
@@ -1703,6 +1713,7 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.pos_env_bytes = round_up(L * 8, 16);
   g.rew_env_bytes = round_up(L * 8, 16);
   g.gd32 = (long long)c.H * c.W > 32767 ? 1 : 0;  // a path is shorter than H * W cells
+  g.gd8 = (long long)c.H * c.W <= 255 ? 1 : 0;
   g.big = (g.N > 64 || c.H > 256 || c.W > 256) ? 1 : 0;
   g.hs_log = 8;
   while ((1 << g.hs_log) < 4 * g.N) ++g.hs_log;
@@ -1887,7 +1898,8 @@ void mapfx_partial_destroy(mapfx_partial_t* h) {
 int32_t mapfx_partial_obs_dim(const mapfx_partial_t* h) { return h ? h->geo.D : -1; }
 
 int32_t mapfx_partial_goal_dist_elem_size(int32_t H, int32_t W) {
-  return (long long)H * W > 32767 ? 4 : 2;
+  const long long hw = (long long)H * W;
+  return hw <= 255 ? 1 : hw > 32767 ? 4 : 2;
 }
 
 int mapfx_partial_goal_dist(mapfx_partial_t* h, const mapfx_partial_state* st,
@@ -1907,9 +1919,9 @@ int mapfx_partial_goal_dist(mapfx_partial_t* h, const mapfx_partial_state* st,
       hipLaunchKernelGGL(partial_bfs_huge_kernel<int16_t>, grid, dim3(HUGE_THREADS), g.huge_lds, sm, g,
                          st->map_bits, st->goal, env_mask, (int16_t*)st->goal_dist);
   } else if (g.H <= 64 && g.W <= 64) {
-    if (g.gd32)  // (not reached: 64 x 64 < 32768 cells)
-      hipLaunchKernelGGL(partial_bfs_kernel<int32_t>, grid, dim3(64), 0, sm, g, st->map_bits, st->goal,
-                         env_mask, (int32_t*)st->goal_dist);
+    if (g.gd8)
+      hipLaunchKernelGGL(partial_bfs_kernel<uint8_t>, grid, dim3(64), 0, sm, g, st->map_bits, st->goal,
+                         env_mask, (uint8_t*)st->goal_dist);
     else
       hipLaunchKernelGGL(partial_bfs_kernel<int16_t>, grid, dim3(64), 0, sm, g, st->map_bits, st->goal,
                          env_mask, (int16_t*)st->goal_dist);
@@ -1917,6 +1929,9 @@ int mapfx_partial_goal_dist(mapfx_partial_t* h, const mapfx_partial_state* st,
     if (g.gd32)
       hipLaunchKernelGGL(partial_bfs_big_kernel<int32_t>, grid, dim3(256), 0, sm, g, st->map_bits,
                          st->goal, env_mask, (int32_t*)st->goal_dist);
+    else if (g.gd8)
+      hipLaunchKernelGGL(partial_bfs_big_kernel<uint8_t>, grid, dim3(256), 0, sm, g, st->map_bits,
+                         st->goal, env_mask, (uint8_t*)st->goal_dist);
     else
       hipLaunchKernelGGL(partial_bfs_big_kernel<int16_t>, grid, dim3(256), 0, sm, g, st->map_bits,
                          st->goal, env_mask, (int16_t*)st->goal_dist);

@@ -113,12 +113,13 @@ class MarlPartialBatch:
         # goal distance of each agent's current cell, carried by the kernels (INT32_MIN:
         # not known yet, looked up; reset / observe set it)
         self.pdist = torch.full((E, N), -2 ** 31, dtype=torch.int32, device=dev)
-        gd_dt = torch.int32 if lib.mapfx_partial_goal_dist_elem_size(self.H, self.W) == 4 \
-            else torch.int16
+        # u8 (255 = -1) while H * W <= 255, int16 up to 32767 cells, else int32
+        gd_dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[
+            int(lib.mapfx_partial_goal_dist_elem_size(self.H, self.W))]
         self.goal_dist = z((E, N, self.H * self.W), gd_dt)
-        # the goal distances of each agent's 4 neighbour cells, carried with pdist (int16
-        # tables only): a step reads a moving agent's npd from it
-        self.pnbr = z((E, N, 4), torch.int16) if gd_dt == torch.int16 else None
+        # the goal distances of each agent's 4 neighbour cells, carried with pdist (u8 /
+        # int16 tables): a step reads a moving agent's npd from it
+        self.pnbr = z((E, N, 4), torch.int16) if gd_dt != torch.int32 else None
         self.out = {k: v[k] for k in ("reward", "obs", "state", "avail")}
         self._state = _abi.PState(
             pos=ptr(self.pos), goal=ptr(self.goal), init_pos=ptr(self.init_pos),

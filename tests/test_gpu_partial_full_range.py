@@ -73,10 +73,14 @@ def _run(mapfx_mod, grids, N, E, T, win, K, seed, crowd=False):
     b = mapfx_mod.MarlPartialBatch(inits, goals, grids=grids, **kw)
     refs = [PartialEnvState(grids[e], inits[e], goals[e], **kw) for e in range(E)]
     H, W = grids.shape[1:]
-    assert b.goal_dist.dtype == (torch.int32 if H * W > 32767 else torch.int16)
+    assert b.goal_dist.dtype == (torch.int32 if H * W > 32767 else torch.uint8 if H * W <= 255
+                                 else torch.int16)
     for e in range(E):
         for a in range(N):
-            assert np.array_equal(_np(b.goal_dist[e, a]).astype(np.int64), refs[e].goal_dist[a]), (e, a)
+            gd = _np(b.goal_dist[e, a]).astype(np.int64)
+            if b.goal_dist.dtype == torch.uint8:
+                gd[gd == 255] = -1          # u8 tables hold -1 as 255
+            assert np.array_equal(gd, refs[e].goal_dist[a]), (e, a)
     out = b.reset()
     assert np.array_equal(_np(out["obs"]), np.stack([r.obs() for r in refs]).astype(np.float32))
     assert np.array_equal(_np(out["avail"]), np.stack([_mask5(r.avail()) for r in refs]))

@@ -2792,7 +2792,10 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     g.wv_off_dep = o;
     o += EPW * g.map_env_bytes;
     g.wv_off_bits = o;
-    o += g.wv_fast ? 0 : EPW * g.wv_bits_env_bytes;  // the fast build reads the bitmap from global
+    // the fast build reads the bitmap words of its rows straight from global memory (one
+    // wide load per lane staged in LDS measured slower: per-step 5.04 -> 6.25 us, C2 T = 20
+    // 21.7 -> 23.8 us, gpurun_out/r05c)
+    o += g.wv_fast ? 0 : EPW * g.wv_bits_env_bytes;
     // rew rows: one double per LANE of the env (every lane writes its slot, +0.0 past
     // N, and the L = 16 fold reads all 16), rounded up to 2 (16 B), +2 doubles so the
     // envs of a wave start on different banks

@@ -303,6 +303,19 @@ __device__ __forceinline__ int gd_entry(const PGeo& g, const void* gd, long long
 __device__ __forceinline__ int goal_dist_at(const PGeo& g, const void* gd, long long oa, int cell) {
   return gd_entry(g, gd, oa * g.hw + cell);
 }
+// the same with the table width known at compile time (GDE bytes: 1 u8, 2 int16; 0: run
+// time): a single load with no branch around it
+template <int GDE>
+__device__ __forceinline__ int gd_entry_t(const PGeo& g, const void* gd, long long i) {
+  if constexpr (GDE == 1) {
+    const int v = ((const uint8_t*)gd)[i];
+    return v == 255 ? -1 : v;
+  } else if constexpr (GDE == 2) {
+    return ((const int16_t*)gd)[i];
+  } else {
+    return gd_entry(g, gd, i);
+  }
+}
 
 // The step's goal-path distances (:227-233) with the current cell's distance carried in
 // the state (mapfx_partial_state.pdist, the reference's _new_pdist of the last step):
@@ -909,7 +922,8 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
 // A block is g.wpb independent waves (no barrier between them): bigger blocks let the
 // dispatcher start the launch's waves sooner (one wave per block took ~1.4 us to have
 // all 1024 waves of the bench shape running).
-template <int WIN, int KF, int LF>
+// GDE: goal-table entry bytes fixed at compile time (1 u8, 2 int16; 0: run time)
+template <int WIN, int KF, int LF, int GDE = 0>
 __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, PArgs a) {
   extern __shared__ __align__(16) unsigned char lds_blk[];
   constexpr int H2 = WIN / 2;
@@ -1083,8 +1097,8 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   int npd_t = 0;
   if (has && !nb_ok) {
     const int tgt = (a.do_step && !dn) ? move_target(g, r, c, act) : -1;
-    if (tgt >= 0) npd_t = goal_dist_at(g, a.gd, oa, tgt);
-    if (need_cur) pd = goal_dist_at(g, a.gd, oa, r * g.W + c);
+    if (tgt >= 0) npd_t = gd_entry_t<GDE>(g, a.gd, oa * g.hw + tgt);
+    if (need_cur) pd = gd_entry_t<GDE>(g, a.gd, oa * g.hw + r * g.W + c);
   }
   PST(3);
   int cur = (r + g.P) * pitch + c + g.pl;
@@ -1211,8 +1225,10 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   // (u8 tables, H * W <= 255: the 4 lookups of an agent fall in one 64-byte table, so one
   // memory request; int16 tables span two)
   const long long gi = oc_ * g.hw + r * g.W + c;
-  const int nbd0 = gd_entry(g, a.gd, gi + (r > 0 ? -g.W : 0)), nbd1 = gd_entry(g, a.gd, gi + (r + 1 < g.H ? g.W : 0));
-  const int nbd2 = gd_entry(g, a.gd, gi + (c > 0 ? -1 : 0)), nbd3 = gd_entry(g, a.gd, gi + (c + 1 < g.W ? 1 : 0));
+  const int nbd0 = gd_entry_t<GDE>(g, a.gd, gi + (r > 0 ? -g.W : 0));
+  const int nbd1 = gd_entry_t<GDE>(g, a.gd, gi + (r + 1 < g.H ? g.W : 0));
+  const int nbd2 = gd_entry_t<GDE>(g, a.gd, gi + (c > 0 ? -1 : 0));
+  const int nbd3 = gd_entry_t<GDE>(g, a.gd, gi + (c + 1 < g.W ? 1 : 0));
 
   PST(8);
   // ---- the step's results leave before the observation rows are built: their stores
@@ -1610,11 +1626,12 @@ int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
   }
   const int blocks = (g.E + g.EPW - 1) / g.EPW;
   void (*fn)(PGeo, PArgs) = nullptr;
-  if (g.K == 5 && g.win == 5 && g.L == 16) fn = partial_kernel<5, 5, 16>;
-  else if (g.K == 5 && g.win == 5 && g.L == 8) fn = partial_kernel<5, 5, 8>;
-  else if (g.K == 5 && g.win == 5 && g.L == 32) fn = partial_kernel<5, 5, 32>;
-  else if (g.K == 5 && g.win == 3 && g.L == 16) fn = partial_kernel<3, 5, 16>;
-  else if (g.K == 5 && g.win == 7 && g.L == 16) fn = partial_kernel<7, 5, 16>;
+  const bool u8 = g.gd8 != 0, i16 = !g.gd8 && !g.gd32;  // the table width, as a template argument
+  if (g.K == 5 && g.win == 5 && g.L == 16) fn = u8 ? partial_kernel<5, 5, 16, 1> : i16 ? partial_kernel<5, 5, 16, 2> : partial_kernel<5, 5, 16>;
+  else if (g.K == 5 && g.win == 5 && g.L == 8) fn = u8 ? partial_kernel<5, 5, 8, 1> : i16 ? partial_kernel<5, 5, 8, 2> : partial_kernel<5, 5, 8>;
+  else if (g.K == 5 && g.win == 5 && g.L == 32) fn = u8 ? partial_kernel<5, 5, 32, 1> : i16 ? partial_kernel<5, 5, 32, 2> : partial_kernel<5, 5, 32>;
+  else if (g.K == 5 && g.win == 3 && g.L == 16) fn = u8 ? partial_kernel<3, 5, 16, 1> : i16 ? partial_kernel<3, 5, 16, 2> : partial_kernel<3, 5, 16>;
+  else if (g.K == 5 && g.win == 7 && g.L == 16) fn = u8 ? partial_kernel<7, 5, 16, 1> : i16 ? partial_kernel<7, 5, 16, 2> : partial_kernel<7, 5, 16>;
   else switch (g.win) {
       case 0: fn = partial_kernel<0, 0, 0>; break;
       case 1: fn = partial_kernel<1, 0, 0>; break;
@@ -1828,7 +1845,11 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
     for (auto fn : {partial_kernel<5, 5, 16>, partial_kernel<5, 5, 8>, partial_kernel<5, 5, 32>,
                     partial_kernel<3, 5, 16>, partial_kernel<7, 5, 16>, partial_kernel<0, 0, 0>,
                     partial_kernel<1, 0, 0>, partial_kernel<3, 0, 0>, partial_kernel<5, 0, 0>,
-                    partial_kernel<7, 0, 0>, partial_kernel<9, 0, 0>})
+                    partial_kernel<7, 0, 0>, partial_kernel<9, 0, 0>,
+                    partial_kernel<5, 5, 16, 1>, partial_kernel<5, 5, 8, 1>, partial_kernel<5, 5, 32, 1>,
+                    partial_kernel<3, 5, 16, 1>, partial_kernel<7, 5, 16, 1>,
+                    partial_kernel<5, 5, 16, 2>, partial_kernel<5, 5, 8, 2>, partial_kernel<5, 5, 32, 2>,
+                    partial_kernel<3, 5, 16, 2>, partial_kernel<7, 5, 16, 2>})
       if (!rc0) rc0 = check_hip(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                     g.lds * g.wpb),
                                 "hipFuncSetAttribute(partial_kernel LDS)");

@@ -1484,7 +1484,7 @@ __device__ __forceinline__ void stage_occ_record(const uint32_t (&R)[(WIN * WIN 
 #endif
 constexpr int SPLIT_WAVES = 3;               // step wave + two store waves
 constexpr int SPLIT_DBM_INFO = 2 * 64 * 16;  // info words of two steps
-constexpr int SPLIT_DBM_EDGE = 2 * 64;       // edge counts of two steps
+constexpr int SPLIT_DBM_EDGE = 3 * 64;       // edge counts of two steps + the launch's last step
 constexpr int SPLIT_FOLD_LDS = 256 * 8 + 32 * 64;  // reward-code table + 32-step code ring
 
 // info.z flag bits
@@ -1595,7 +1595,9 @@ __device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a
     u32x4 rv[NRC];
 #pragma unroll
     for (int k = 0; k < NRC; ++k) rv[k] = ost[(k < NRC - 1 || lane + 64 * k < RCH) ? lane + 64 * k : 0];
-    const uint32_t edge = ering[(q & 1) * 64 + lane];
+    // (the last step's count has its own slot: the step wave writes it while b(T - 3) may
+    // still read slot (T - 1) & 1)
+    const uint32_t edge = ering[(q + 1 == (uint32_t)T ? 2u : (q & 1)) * 64 + lane];
     codes[(q & 31) * 64 + lane] =
         (unsigned char)(k_node | (k_fl & (SF_LIVE | SF_DNOLD | SF_ENVC)) | ((edge & 0xFu) << 4));
     gbyte* rec = (gbyte*)(OCC ? a.obs_window_occ : a.obs_window) + (q * EN + ag0) * (uint32_t)REC;
@@ -1627,7 +1629,10 @@ __device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a
     }
   };
 
-  const int rounds = T > 0 ? T + 1 : 0;
+  // T rounds: the launch's last step has its edge count published with its info word
+  // (barrier T), so its wave runs a(T - 1) and b(T - 1) back to back in the last interval
+  // instead of spending one more barrier interval on b(T - 1) alone
+  const int rounds = T > 0 ? T : 0;
   for (int s = 1; s <= rounds; ++s) {
 #ifdef MAPFX_STAMPS  // diagnostic: end of round s - 1's work (columns 5 / 7 of row s - 1)
     if (s > 1) {
@@ -1638,8 +1643,15 @@ __device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a
 #endif
     split_barrier();
     const int q = s - 1;  // a(q) now; b(q - 1) by the other parity
-    if (q < T && (q & 1) == par) part_a((uint32_t)q);
-    else if (q >= 1 && ((q - 1) & 1) == par) part_b((uint32_t)(q - 1));
+    if ((q & 1) == par) {
+      part_a((uint32_t)q);
+      if (q == T - 1) {  // the last step: its b part right away (own staged record: LDS order)
+        wave_fence();
+        part_b((uint32_t)q);
+      }
+    } else if (q >= 1) {
+      part_b((uint32_t)(q - 1));
+    }
   }
 }
 
@@ -2108,6 +2120,10 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
       q_dj = dj;
       q_moved = moved;
       nb = nbn;
+      if (s == T - 1) {  // the last step's edge count now (slot 2): its b part runs next interval
+        const int e = edge_of();
+        ering[2 * 64 + lane64] = (unsigned char)(e > 255 ? 255 : e);
+      }
       if (a.autoreset && alldone) {  // counted at init_pos in the next step's map
         const int2 p = ((const int2*)a.init_pos)[oa];
         cur = cell0 + p.x * pitch + p.y;
@@ -2120,11 +2136,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
       split_barrier();  // info s, map s & 1, edge s - 1 -> store waves
       STAMP(6);
     }
-    if (T > 0) {  // the last step's edge count
-      const int e = edge_of();
-      ering[((T - 1) & 1) * 64 + lane64] = (unsigned char)(e > 255 ? 255 : e);
-    }
-    split_barrier();
     ((int2*)a.pos)[oa] = cell_rc(cur);
     a.done[oa] = dn ? 1 : 0;
     if (a.steps) a.steps[oa] = st;

@@ -970,3 +970,27 @@ def test_generic_rollout_every_step(mapfx_mod, S, N, E, T, p, obs):
     if S == 24:
         assert max_edge >= 4, max_edge
     assert np.array_equal(_np(b1.steps), _np(b2.steps))
+
+
+def test_last_kernel_names_the_launched_instance(mapfx_mod):
+    """mapfx_last_kernel (ABI 5) names the env kernel each entry point launched, as
+    rocprofv3 does: what bench.py records and checks a profile against."""
+    from mapfx import _abi
+    from mapfx.maps import synthetic_instances
+    inst = synthetic_instances(8, 8, 8, 4, p_obstacle=0.1, seed=3)
+    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(8, 8),
+                                obs=("window",), window=5)
+    b.reset()
+    b.step(torch.full((8, 4), 4, dtype=torch.int8, device="cuda"))
+    assert _abi.last_kernel().startswith("void (anonymous namespace)::mapf_wave_kernel<5, false"), \
+        _abi.last_kernel()
+    p = mapfx_mod.MarlPartialBatch(inst["init_pos"], inst["goals"], grids=inst["grid"][:1])
+    p.reset()
+    p.step(torch.full((8, 4), 4, dtype=torch.int64, device="cuda"))
+    assert "partial_kernel<" in _abi.last_kernel(), _abi.last_kernel()
+    q = mapfx_mod.PrimalBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(8, 8),
+                              observation_size=5)
+    q.act(torch.ones((8, 2), dtype=torch.int32, device="cuda"),
+          torch.full((8, 2), 4, dtype=torch.int32, device="cuda"))
+    assert "primal_" in _abi.last_kernel() and "<" in _abi.last_kernel(), _abi.last_kernel()
+    assert _abi.build_id().startswith("src=")

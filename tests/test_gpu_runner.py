@@ -131,12 +131,13 @@ class TiledMAC:
         return torch.where(ok, a, torch.full_like(a, 4))
 
 
-@pytest.mark.parametrize("B", [4096, 1100])
+@pytest.mark.parametrize("B", [4096, 4100, 1100, 1102])
 @pytest.mark.parametrize("name", CASES)
 def test_runner_tiled_matches_reference_at_bench_shape(tmp_path, name, B):
     """the runner's multi-wave `bs` compaction (runner.hip, per-thread
     chunks + wave scans, reached only at large B) pinned at the bench's B = 4096 and
-    at a ragged B = 1100.  Every env of the batch is the fixture instance and acts
+    at ragged sizes (1100; 1102, not a multiple of 4; 4100, whose per-thread chunks of
+    5 envs leave the last threads empty).  Every env of the batch is the fixture instance and acts
     as fixture env b % B_fx, so env b's rows must equal the REFERENCE runner's rows
     of env b % B_fx byte for byte (envs never interact), every run.  Per-env returns
     and lengths must equal those of the B_fx-env run (itself pinned to the fixture's

@@ -558,14 +558,25 @@ def kernel_instance(name):
     return (name[:j] if j > 0 else name).strip()
 
 
+def build_src(build_id):
+    """The `src=<hash>` part of a build id ("src=<hash> git=<head>[+dirty]"), or None."""
+    for part in (build_id or "").split():
+        if part.startswith("src=") and part != "src=unknown":
+            return part
+    return None
+
+
 def profile_traffic(leg, kernel=None, path=None, **match):
     """(traffic bytes per launch, source) from profiles/pmc_<leg>.json, or (None, why).
     The file is written by tools/pmc_traffic.py from separate rocprofv3 FETCH_SIZE /
     WRITE_SIZE passes (MI355X_MICROARCH.md corrections).  It is cited only when it was
-    taken of THIS build (its build_id equals mapfx_build_id of the loaded library), of
-    the same kernel instance the bench just launched (`kernel`, mapfx_last_kernel) and
-    of this workload (every `match` key equal); otherwise traffic is null and the
-    reason is reported instead of a stale figure."""
+    taken of THIS kernel code (the `src=` hash of its build_id -- the HIP sources,
+    headers and compiler flags -- equals that of the loaded library; the `git=` part
+    records the commit it was built at and is reported, not compared: rebuilding the
+    same sources at a later commit gives the same kernels), of the same kernel instance
+    the bench just launched (`kernel`, mapfx_last_kernel) and of this workload (every
+    `match` key equal); otherwise traffic is null and the reason is reported instead
+    of a stale figure."""
     from mapfx import _abi
     path = path or os.path.join(REPO, "profiles", "pmc_%s.json" % leg)
     rel = os.path.relpath(path, REPO)
@@ -574,7 +585,7 @@ def profile_traffic(leg, kernel=None, path=None, **match):
             pm = json.load(f)
     except (OSError, ValueError):
         return None, "no profile %s" % rel
-    if pm.get("build_id") != _abi.build_id():
+    if build_src(pm.get("build_id")) is None or build_src(pm.get("build_id")) != build_src(_abi.build_id()):
         return None, "refused %s: taken of build %r, running %r" % (rel, pm.get("build_id"),
                                                                     _abi.build_id())
     if kernel is not None and kernel_instance(pm.get("kernel", "")) != kernel_instance(kernel):
@@ -582,7 +593,8 @@ def profile_traffic(leg, kernel=None, path=None, **match):
     bad = [k for k, v in match.items() if pm.get(k) != v]
     if bad or not pm.get("traffic_bytes_per_launch"):
         return None, "refused %s: workload keys %s differ" % (rel, bad)
-    return pm["traffic_bytes_per_launch"], "%s: %s" % (rel, pm.get("command", "rocprofv3 --pmc passes"))
+    return pm["traffic_bytes_per_launch"], "%s (build %s): %s" % (rel, pm.get("build_id"),
+                                                                  pm.get("command", "rocprofv3 --pmc passes"))
 
 
 def partial_bytes_per_env_step(N, D, HW, gd_bytes=2):

@@ -1,7 +1,9 @@
 """bench.py cites a PMC profile's traffic only when the profile was taken of the
-running build (mapfx_build_id), of the kernel instance the bench launched
-(mapfx_last_kernel) and of the same workload; otherwise traffic is null and the
-reason is reported (a profile of a superseded build had been cited)."""
+running kernel code (the src= hash of mapfx_build_id: HIP sources, headers and
+flags), of the kernel instance the bench launched (mapfx_last_kernel) and of the
+same workload; otherwise traffic is null and the reason is reported (a
+profile of a superseded build had been cited).  The git= part of the build id only
+records where the library was built."""
 import json
 import os
 
@@ -33,8 +35,18 @@ def test_profile_of_this_build_and_kernel_is_cited(bench_mod, tmp_path):
     assert t == 123 and src.endswith("cmd")
 
 
+def test_same_sources_built_at_another_commit_are_cited(bench_mod, tmp_path):
+    from mapfx import _abi
+    src_part = _abi.build_id().split()[0]
+    p = _write(tmp_path, build_id=src_part + " git=0123456789ab", kernel=K, config="c2", T=20,
+               E=4096, traffic_bytes_per_launch=7, command="cmd")
+    t, src = bench_mod.profile_traffic("x", kernel=K, path=p, config="c2", T=20, E=4096)
+    assert t == 7 and "git=0123456789ab" in src
+
+
 @pytest.mark.parametrize("field,value,why", [
     ("build_id", "src=0000000000000000 git=deadbeef", "taken of build"),
+    ("build_id", "src=unknown git=unknown", "taken of build"),
     ("kernel", K.replace("false, 8>", "false, 0>"), "profiled kernel"),
     ("T", 64, "workload keys"),
 ])

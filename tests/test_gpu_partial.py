@@ -262,7 +262,7 @@ def test_partial_carried_distances_equal_lookup(mapfx_mod):
     lookup = mapfx_mod.MarlPartialBatch(inits, goals, grids=grid[None], **kw)
     lookup._state.pdist = None
     lookup._state.pnbr = None
-    assert carried.pnbr is not None          # int16 tables: the carried path is on
+    assert carried.pnbr is not None          # u8 tables (144 cells): the carried path is on
     refs = [PartialEnvState(grid, inits[e], goals[e], **kw) for e in range(E)]
     carried.reset()
     lookup.reset()

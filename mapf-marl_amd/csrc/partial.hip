@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <new>
+#include <vector>
 
 #include "internal.h"
 #include "mapfx.h"
@@ -923,7 +924,9 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
 // dispatcher start the launch's waves sooner (one wave per block took ~1.4 us to have
 // all 1024 waves of the bench shape running).
 // GDE: goal-table entry bytes fixed at compile time (1 u8, 2 int16; 0: run time)
-template <int WIN, int KF, int LF, int GDE = 0>
+// RUN: the runner's fused actions / post pass compiled in (false: the plain step, whose
+// code then holds none of the runner's pointers: 2043 -> 1747 VALU instructions)
+template <int WIN, int KF, int LF, int GDE = 0, bool RUN = true>
 __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, PArgs a) {
   extern __shared__ __align__(16) unsigned char lds_blk[];
   constexpr int H2 = WIN / 2;
@@ -960,8 +963,8 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   // the prologue ----
   const long long oc_ = has ? oa : 0;
   const int ec_ = env_ok ? env : 0;
-  const bool runner = a.do_step && a.ra.act_row != nullptr;
-  const bool post = a.ra.alive != nullptr;  // the runner's post pass, fused
+  const bool runner = RUN && a.do_step && a.ra.act_row != nullptr;
+  const bool post = RUN && a.ra.alive != nullptr;  // the runner's post pass, fused
   const bool nb_carry = a.pnbr && a.pdist && !g.gd32;  // neighbour distances carried
   const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared ? 0 : (long long)ec_ * g.map_stride));
   const uint32_t bw0 = bsrc[ag < g.bits_words ? ag : 0];  // this lane's first bitmap word
@@ -1235,7 +1238,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   // then queue ahead of the rows' copy-out instead of behind it ----
   // avail (:399-433): neighbour in bounds and not a free-standing obstacle
   uint32_t am = 16u;
-  if (has && (a.avail || a.ra.ep_avail)) {
+  if (has && (a.avail || (RUN && a.ra.ep_avail))) {
     if (map[cur - pitch]) am |= 1u;
     if (map[cur + pitch]) am |= 2u;
     if (map[cur - 1]) am |= 4u;
@@ -1612,6 +1615,15 @@ void (*pick_wg(int win, int apl))(PGeo, PArgs) {
 
 int wg_apl(const PGeo& g) { return (g.N + WG_THREADS - 1) / WG_THREADS; }
 
+// the fast-path instance: table width (u8 / int16 / run time) x runner fusion
+template <int WIN, int LF>
+void (*pick_fast(bool u8, bool i16, bool run))(PGeo, PArgs) {
+  if (run) return u8 ? partial_kernel<WIN, 5, LF, 1, true> : i16 ? partial_kernel<WIN, 5, LF, 2, true>
+                                                              : partial_kernel<WIN, 5, LF, 0, true>;
+  return u8 ? partial_kernel<WIN, 5, LF, 1, false> : i16 ? partial_kernel<WIN, 5, LF, 2, false>
+                                                         : partial_kernel<WIN, 5, LF, 0, false>;
+}
+
 int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
   const PGeo& g = h->geo;
   if (g.E == 0) return MAPFX_OK;
@@ -1627,11 +1639,12 @@ int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
   const int blocks = (g.E + g.EPW - 1) / g.EPW;
   void (*fn)(PGeo, PArgs) = nullptr;
   const bool u8 = g.gd8 != 0, i16 = !g.gd8 && !g.gd32;  // the table width, as a template argument
-  if (g.K == 5 && g.win == 5 && g.L == 16) fn = u8 ? partial_kernel<5, 5, 16, 1> : i16 ? partial_kernel<5, 5, 16, 2> : partial_kernel<5, 5, 16>;
-  else if (g.K == 5 && g.win == 5 && g.L == 8) fn = u8 ? partial_kernel<5, 5, 8, 1> : i16 ? partial_kernel<5, 5, 8, 2> : partial_kernel<5, 5, 8>;
-  else if (g.K == 5 && g.win == 5 && g.L == 32) fn = u8 ? partial_kernel<5, 5, 32, 1> : i16 ? partial_kernel<5, 5, 32, 2> : partial_kernel<5, 5, 32>;
-  else if (g.K == 5 && g.win == 3 && g.L == 16) fn = u8 ? partial_kernel<3, 5, 16, 1> : i16 ? partial_kernel<3, 5, 16, 2> : partial_kernel<3, 5, 16>;
-  else if (g.K == 5 && g.win == 7 && g.L == 16) fn = u8 ? partial_kernel<7, 5, 16, 1> : i16 ? partial_kernel<7, 5, 16, 2> : partial_kernel<7, 5, 16>;
+  const bool run = a.ra.act_row != nullptr || a.ra.alive != nullptr;  // the runner's fused step
+  if (g.K == 5 && g.win == 5 && g.L == 16) fn = pick_fast<5, 16>(u8, i16, run);
+  else if (g.K == 5 && g.win == 5 && g.L == 8) fn = pick_fast<5, 8>(u8, i16, run);
+  else if (g.K == 5 && g.win == 5 && g.L == 32) fn = pick_fast<5, 32>(u8, i16, run);
+  else if (g.K == 5 && g.win == 3 && g.L == 16) fn = pick_fast<3, 16>(u8, i16, run);
+  else if (g.K == 5 && g.win == 7 && g.L == 16) fn = pick_fast<7, 16>(u8, i16, run);
   else switch (g.win) {
       case 0: fn = partial_kernel<0, 0, 0>; break;
       case 1: fn = partial_kernel<1, 0, 0>; break;
@@ -1842,14 +1855,18 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
     }
   } else if (g.lds * g.wpb > 64 * 1024) {
     int rc0 = MAPFX_OK;
-    for (auto fn : {partial_kernel<5, 5, 16>, partial_kernel<5, 5, 8>, partial_kernel<5, 5, 32>,
-                    partial_kernel<3, 5, 16>, partial_kernel<7, 5, 16>, partial_kernel<0, 0, 0>,
-                    partial_kernel<1, 0, 0>, partial_kernel<3, 0, 0>, partial_kernel<5, 0, 0>,
-                    partial_kernel<7, 0, 0>, partial_kernel<9, 0, 0>,
-                    partial_kernel<5, 5, 16, 1>, partial_kernel<5, 5, 8, 1>, partial_kernel<5, 5, 32, 1>,
-                    partial_kernel<3, 5, 16, 1>, partial_kernel<7, 5, 16, 1>,
-                    partial_kernel<5, 5, 16, 2>, partial_kernel<5, 5, 8, 2>, partial_kernel<5, 5, 32, 2>,
-                    partial_kernel<3, 5, 16, 2>, partial_kernel<7, 5, 16, 2>})
+    std::vector<void (*)(PGeo, PArgs)> fns = {partial_kernel<0, 0, 0>, partial_kernel<1, 0, 0>,
+                                              partial_kernel<3, 0, 0>, partial_kernel<5, 0, 0>,
+                                              partial_kernel<7, 0, 0>, partial_kernel<9, 0, 0>};
+    for (int t = 0; t < 6; ++t) {  // every fast instance
+      const bool u8 = t % 3 == 0, i16 = t % 3 == 1, run = t >= 3;
+      fns.push_back(pick_fast<5, 16>(u8, i16, run));
+      fns.push_back(pick_fast<5, 8>(u8, i16, run));
+      fns.push_back(pick_fast<5, 32>(u8, i16, run));
+      fns.push_back(pick_fast<3, 16>(u8, i16, run));
+      fns.push_back(pick_fast<7, 16>(u8, i16, run));
+    }
+    for (auto fn : fns)
       if (!rc0) rc0 = check_hip(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                     g.lds * g.wpb),
                                 "hipFuncSetAttribute(partial_kernel LDS)");

@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <new>
+#include <type_traits>
 #include <vector>
 
 #include "internal.h"
@@ -112,6 +113,7 @@ struct PGeo {
   long long map_stride;
   int map_env_bytes, bits_env_bytes, feat_env_bytes, pos_env_bytes, rew_env_bytes, stage_env_bytes, stage_lanes;
   int off_map, off_dep, off_bits, off_feat, off_pos, off_rew, off_stage, lds;  // off_stage < 0: none
+  int off_sqrt;                      // float32 sqrt(0 .. sq_max) per wave (fast path), < 0: none
   int win, K, D, limit, hw;          // window, knn, obs dim, episode limit, H*W
   double move_rew, stay_rew, stay_goal_rew, nc_rew, ec_rew, env_rew;
   int sq_max, bonus_len;             // LUT sizes
@@ -163,8 +165,9 @@ struct PArgs {
 
 // where env e's observation rows go ([N][D] floats), or nullptr when not written
 // (partial_kernel: the caller has read obs_mask[e] with the launch's other loads)
+template <bool ROWS = true>
 __device__ __forceinline__ float* obs_env_nomask(const PArgs& a, int e, int D, int N) {
-  if (a.obs_rows) return a.obs_rows + (long long)e * a.obs_env_stride;
+  if (ROWS && a.obs_rows) return a.obs_rows + (long long)e * a.obs_env_stride;
   return a.obs ? a.obs + (long long)e * N * D : nullptr;
 }
 __device__ __forceinline__ float* obs_env(const PArgs& a, int e, int D, int N) {
@@ -924,8 +927,9 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
 // dispatcher start the launch's waves sooner (one wave per block took ~1.4 us to have
 // all 1024 waves of the bench shape running).
 // GDE: goal-table entry bytes fixed at compile time (1 u8, 2 int16; 0: run time)
-// RUN: the runner's fused actions / post pass compiled in (false: the plain step, whose
-// code then holds none of the runner's pointers: 2043 -> 1747 VALU instructions)
+// RUN: the runner's fused actions / post pass and EpisodeBatch observation rows compiled
+// in (false: the plain step, whose code then holds none of the runner's pointers: 2043
+// -> 1747 VALU instructions)
 template <int WIN, int KF, int LF, int GDE = 0, bool RUN = true>
 __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, PArgs a) {
   extern __shared__ __align__(16) unsigned char lds_blk[];
@@ -993,7 +997,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   const int t0 = a.t[ec_], total0 = a.total_coll[ec_];
   const uint8_t term0 = a.terminated[ec_];
   uint32_t om_raw = 1, rm_raw = 1, live_raw = 0;
-  if (a.obs_rows && a.obs_mask) om_raw = a.obs_mask[ec_];
+  if (RUN && a.obs_rows && a.obs_mask) om_raw = a.obs_mask[ec_];
   if (a.do_reset && a.reset_mask) rm_raw = a.reset_mask[ec_];
   double epr_raw = 0.0;
   int64_t epl_raw = 0;
@@ -1001,6 +1005,13 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
     live_raw = a.ra.alive[ec_];
     epr_raw = a.ra.ep_return[ec_];
     epl_raw = a.ra.ep_length[ec_];
+  }
+  if constexpr (KF > 0 && LF > 0) {  // float32 sqrt(0 .. sq_max) for the K-nearest rows
+    if (g.off_sqrt >= 0) {            // (:352 math.sqrt), while the loads are in flight
+      float* sqt = (float*)(lds + g.off_sqrt);
+#pragma unroll 1
+      for (int i = lane64; i <= g.sq_max; i += 64) sqt[i] = (float)isqrt_f64(i);
+    }
   }
   // ---- LDS map (c format) + dep map (obstacle flag in bit 7) ----
   // (staging the bitmap before the state loads are issued measured slower: 15.73 vs
@@ -1324,7 +1335,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   constexpr int WW = WIN * WIN;
   constexpr int DF = (KF > 0 && LF > 0) ? 2 * WW + NF * KF : 1;  // fast-path row length
   float o[DF];
-  float* const my_obs = (env_ok && omask) ? obs_env_nomask(a, env, (KF > 0 && LF > 0) ? DF : g.D, N) : nullptr;
+  float* const my_obs = (env_ok && omask) ? obs_env_nomask<RUN>(a, env, (KF > 0 && LF > 0) ? DF : g.D, N) : nullptr;
   // Staged copy-out (fast path): the rows of the envs of a staging group (the whole wave,
   // or each half of it) are one contiguous run of the destination (a.obs), or one run
   // per env (EpisodeBatch rows): each run is staged in LDS as its byte image, at the
@@ -1333,8 +1344,8 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
   // regions the step is done with (dep onwards).  (Sending the window planes first, while
   // the K-nearest rows are built, measured 19.0 vs 15.2 us: chunks of partial lines.)
   constexpr bool FAST = KF > 0 && LF > 0;
-  const bool one_run = a.obs_rows == nullptr;
-  const bool staged = FAST && (a.obs || a.obs_rows) && g.off_stage >= 0;
+  const bool one_run = !RUN || a.obs_rows == nullptr;
+  const bool staged = FAST && (a.obs || (RUN && a.obs_rows)) && g.off_stage >= 0;
   // this lane's row of group gi's image (G lanes per group)
   auto stage_row = [&](int gi, int G, int i0, int i1) {
     const int s0 = (G * gi) >> g.lshift;
@@ -1434,33 +1445,39 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
       for (int q = 0; q < 11; ++q) k0[q] = me[q];
       k0[11] = (float)(g.H * g.W);  // distance to itself (:543-545)
       k0[12] = me[11];
-      uint32_t prev = 0u;
-      bool first = true;
+      // round sI takes the smallest key above the last one: keys are distinct, so with
+      // prev1 = last + 1 every key <= last wraps to ~2^32 in key - prev1 (an unused
+      // slot's 0xFFFFFFFF stays above every real key) and one min over key - prev1 finds
+      // it -- a subtract and a third of a min3 per key (was compare, compare, select)
+      uint32_t prev1 = 0u;
+      const float* sqt = (const float*)(lds + (g.off_sqrt >= 0 ? g.off_sqrt : 0));
       // (a branch per round measured faster than computing every round and selecting -1:
       // 15.2 vs 16.2 us)
+      const auto rounds = [&](auto lut) {  // lut: the distances from the wave's table
 #pragma unroll
-      for (int sI = 1; sI < KF; ++sI) {
-        float* row = o + 2 * WW + sI * NF;
-        if (sI <= km1) {
-          uint32_t best = 0xFFFFFFFFu;
+        for (int sI = 1; sI < KF; ++sI) {
+          float* row = o + 2 * WW + sI * NF;
+          if (sI <= km1) {
+            uint32_t m = 0xFFFFFFFFu;
 #pragma unroll
-          for (int j = 0; j < LF; ++j) {
-            const uint32_t kj = key[j];
-            best = (kj < best && (first || kj > prev)) ? kj : best;
+            for (int j = 0; j < LF; ++j) m = min(m, key[j] - prev1);
+            const uint32_t best = m + prev1;
+            prev1 = best + 1u;
+            const int j = (int)(best & 63u);
+            const float* fj = feat + j * FR;
+#pragma unroll
+            for (int q = 0; q < 11; ++q) row[q] = fj[q];
+            if constexpr (decltype(lut)::value) row[11] = sqt[best >> 6];
+            else row[11] = (float)isqrt_f64((int)(best >> 6));
+            row[12] = fj[11];
+          } else {
+#pragma unroll
+            for (int q = 0; q < NF; ++q) row[q] = -1.0f;
           }
-          first = false;
-          prev = best;
-          const int j = (int)(best & 63u);
-          const float* fj = feat + j * FR;
-#pragma unroll
-          for (int q = 0; q < 11; ++q) row[q] = fj[q];
-          row[11] = (float)isqrt_f64((int)(best >> 6));
-          row[12] = fj[11];
-        } else {
-#pragma unroll
-          for (int q = 0; q < NF; ++q) row[q] = -1.0f;
         }
-      }
+      };
+      if (g.off_sqrt >= 0) rounds(std::true_type{});
+      else rounds(std::false_type{});
     } else {
       // -------- generic path --------
       float* o = my_obs + ag * g.D;
@@ -1639,7 +1656,8 @@ int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
   const int blocks = (g.E + g.EPW - 1) / g.EPW;
   void (*fn)(PGeo, PArgs) = nullptr;
   const bool u8 = g.gd8 != 0, i16 = !g.gd8 && !g.gd32;  // the table width, as a template argument
-  const bool run = a.ra.act_row != nullptr || a.ra.alive != nullptr;  // the runner's fused step
+  // the runner's fused step, or observation rows to an EpisodeBatch time row
+  const bool run = a.ra.act_row != nullptr || a.ra.alive != nullptr || a.obs_rows != nullptr;
   if (g.K == 5 && g.win == 5 && g.L == 16) fn = pick_fast<5, 16>(u8, i16, run);
   else if (g.K == 5 && g.win == 5 && g.L == 8) fn = pick_fast<5, 8>(u8, i16, run);
   else if (g.K == 5 && g.win == 5 && g.L == 32) fn = pick_fast<5, 32>(u8, i16, run);
@@ -1800,6 +1818,14 @@ int mapfx_partial_create(const mapfx_partial_cfg* cfg, mapfx_partial_t** out) {
   g.off_feat = off; off += EPW * g.feat_env_bytes;
   g.off_pos = off; off += EPW * g.pos_env_bytes;
   g.off_rew = off; off += EPW * g.rew_env_bytes;
+  // the K-nearest rows' distances sqrt(0 .. sq_max) as float32, one table per wave filled
+  // while the state loads are in flight (small maps: sq_max < 512, i.e. sides up to 16)
+  g.off_sqrt = -1;
+  const long long sq_max_ = 2ll * (std::max(c.H, c.W) - 1) * (std::max(c.H, c.W) - 1);  // = g.sq_max below
+  if (sq_max_ < 512) {
+    g.off_sqrt = off;
+    off += round_up((int)(sq_max_ + 1) * 4, 16);
+  }
   // the fast observation path's staging images (one env's rows + 16 bytes of alignment
   // slack each) for a group of 64 lanes (the whole wave) or 32 (each half in turn),
   // aliasing dep onwards; the whole wave while the block stays within 40 KB (4 blocks

@@ -1,9 +1,10 @@
 #!/bin/bash
-# Round 5, call R: the partial kernel with the runner's fusion as a template argument (the
+# Round 5, call R (and S: the K-nearest selection by one min per round over key - (last + 1)
+# and a per-wave float32 sqrt table): the partial kernel with the runner fusion as a template argument (the
 # plain step compiled without it) against the previous build (varlibs/libmapfx_old.so):
 # MARL_PARTIAL and runner bench lines interleaved, then the partial / runner GPU tests.
 set -o pipefail
-O=gpurun_out/r05r
+O=gpurun_out/${OUT:-r05r}
 mkdir -p $O
 for rep in 1 2 3; do
   for v in new old; do

@@ -559,10 +559,30 @@ def kernel_instance(name):
 
 
 def build_src(build_id):
-    """The `src=<hash>` part of a build id ("src=<hash> git=<head>[+dirty]"), or None."""
+    """The `src=<hash>` part of a build id ("src=<hash> git=<head>[+dirty] tu=..."), or None."""
     for part in (build_id or "").split():
         if part.startswith("src=") and part != "src=unknown":
             return part
+    return None
+
+
+def kernel_unit(kernel):
+    """The translation unit (mapf-marl_amd/csrc/<unit>.hip) that defines a kernel."""
+    base = kernel_instance(kernel or "").split("<")[0].split("::")[-1].strip()
+    for pre, unit in (("partial_", "partial"), ("primal_", "primal"), ("runner_", "runner")):
+        if base.startswith(pre):
+            return unit
+    return "mapfx"
+
+
+def build_unit(build_id, unit):
+    """The hash of one translation unit in a build id's `tu=` part, or None."""
+    for part in (build_id or "").split():
+        if part.startswith("tu="):
+            for item in part[3:].split(","):
+                name, _, h = item.partition(":")
+                if name == unit and h:
+                    return h
     return None
 
 
@@ -571,9 +591,11 @@ def profile_traffic(leg, kernel=None, path=None, **match):
     The file is written by tools/pmc_traffic.py from separate rocprofv3 FETCH_SIZE /
     WRITE_SIZE passes (MI355X_MICROARCH.md corrections).  It is cited only when it was
     taken of THIS kernel code (the `src=` hash of its build_id -- the HIP sources,
-    headers and compiler flags -- equals that of the loaded library; the `git=` part
-    records the commit it was built at and is reported, not compared: rebuilding the
-    same sources at a later commit gives the same kernels), of the same kernel instance
+    headers and compiler flags -- equals that of the loaded library, or the `tu=` hash
+    of the translation unit that defines the kernel does: its source, the headers and
+    its flags; the `git=` part records the commit it was built at and is reported, not
+    compared: rebuilding the same sources at a later commit gives the same kernels), of
+    the same kernel instance
     the bench just launched (`kernel`, mapfx_last_kernel) and of this workload (every
     `match` key equal); otherwise traffic is null and the reason is reported instead
     of a stale figure."""
@@ -585,7 +607,12 @@ def profile_traffic(leg, kernel=None, path=None, **match):
             pm = json.load(f)
     except (OSError, ValueError):
         return None, "no profile %s" % rel
-    if build_src(pm.get("build_id")) is None or build_src(pm.get("build_id")) != build_src(_abi.build_id()):
+    same_src = build_src(pm.get("build_id")) is not None and \
+        build_src(pm.get("build_id")) == build_src(_abi.build_id())
+    unit = kernel_unit(kernel or pm.get("kernel"))
+    same_unit = build_unit(pm.get("build_id"), unit) is not None and \
+        build_unit(pm.get("build_id"), unit) == build_unit(_abi.build_id(), unit)
+    if not (same_src or same_unit):
         return None, "refused %s: taken of build %r, running %r" % (rel, pm.get("build_id"),
                                                                     _abi.build_id())
     if kernel is not None and kernel_instance(pm.get("kernel", "")) != kernel_instance(kernel):

@@ -44,6 +44,34 @@ def test_same_sources_built_at_another_commit_are_cited(bench_mod, tmp_path):
     assert t == 7 and "git=0123456789ab" in src
 
 
+def test_same_unit_other_units_changed_is_cited(bench_mod, tmp_path):
+    """A profile stays valid when only OTHER translation units changed: the tu= hash of
+    the unit that defines the kernel (mapfx.hip for mapf_wave_kernel) matches."""
+    from mapfx import _abi
+    bid = _abi.build_id()
+    tu = [p for p in bid.split() if p.startswith("tu=")][0]
+    items = dict(i.split(":") for i in tu[3:].split(","))
+    items["partial"] = "0" * 12                     # another unit differs
+    other = "src=ffffffffffffffff git=abc tu=" + ",".join("%s:%s" % kv for kv in items.items())
+    p = _write(tmp_path, build_id=other, kernel=K, config="c2", T=20, E=4096,
+               traffic_bytes_per_launch=9, command="cmd")
+    t, src = bench_mod.profile_traffic("x", kernel=K, path=p, config="c2", T=20, E=4096)
+    assert t == 9
+    items["mapfx"] = "1" * 12                       # the kernel's own unit differs
+    other = "src=ffffffffffffffff git=abc tu=" + ",".join("%s:%s" % kv for kv in items.items())
+    p = _write(tmp_path, build_id=other, kernel=K, config="c2", T=20, E=4096,
+               traffic_bytes_per_launch=9, command="cmd")
+    t, src = bench_mod.profile_traffic("x", kernel=K, path=p, config="c2", T=20, E=4096)
+    assert t is None and "taken of build" in src
+
+
+def test_kernel_units():
+    import bench
+    assert bench.kernel_unit("void (anonymous namespace)::partial_kernel<5, 5, 16, 1, false>(a)") == "partial"
+    assert bench.kernel_unit(K) == "mapfx"
+    assert bench.kernel_unit("void (anonymous namespace)::primal_seq_kernel<10, false>(x)") == "primal"
+
+
 @pytest.mark.parametrize("field,value,why", [
     ("build_id", "src=0000000000000000 git=deadbeef", "taken of build"),
     ("build_id", "src=unknown git=unknown", "taken of build"),

@@ -271,6 +271,18 @@ __device__ __forceinline__ void fold_from(double& R, double x, int N) {
     fold_from<K + 1>(R, x, N);
   }
 }
+// The same fold over a lane group of LG lanes known at compile time: every lane of the
+// group past the env's N agents holds 0.0, and R is never -0.0 (it starts as 0.0 + r[0],
+// and in round-to-nearest a sum is -0.0 only when both terms are), so R + 0.0 == R
+// exactly and all LG - 1 shifts are folded with no per-term test of N (which cost a
+// branch per term)
+template <int K, int LG>
+__device__ __forceinline__ void fold_all(double& R, double x) {
+  if constexpr (K < LG) {
+    R = R + row_shl_f64<K>(x);
+    fold_all<K + 1, LG>(R, x);
+  }
+}
 // edge collisions against every other lane of a 16-lane row (lane i sees lane (i + k) % 16
 // for k = 1..15; lanes past N hold an unmoved cell and never match a moving agent)
 template <int K>
@@ -281,9 +293,12 @@ __device__ __forceinline__ void dpp_edge_scan(int cur, int nc, int& e) {
     dpp_edge_scan<K + 1>(cur, nc, e);
   }
 }
+// LG: the lane group when known at compile time (lanes past N must then hold 0.0), else 0
+template <int LG>
 __device__ __forceinline__ double row_fold(double x, int N) {
   double R = 0.0 + x;
-  fold_from<1>(R, x, N);
+  if constexpr (LG > 0 && LG <= 16) fold_all<1, LG>(R, x);
+  else fold_from<1>(R, x, N);
   return R;
 }
 
@@ -931,7 +946,13 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
 // in (false: the plain step, whose code then holds none of the runner's pointers: 2043
 // -> 1747 VALU instructions)
 template <int WIN, int KF, int LF, int GDE = 0, bool RUN = true>
-__global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, PArgs a) {
+__global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g_, PArgs a) {
+  PGeo g = g_;
+  if constexpr (LF > 0) {  // the fast instances' lane group and K as constants (launch() picks
+    g.L = LF;              // them only for g.L == LF, g.K == KF)
+    g.lshift = __builtin_ctz(LF);
+    g.K = KF;
+  }
   extern __shared__ __align__(16) unsigned char lds_blk[];
   constexpr int H2 = WIN / 2;
   const int lane64 = threadIdx.x & 63;
@@ -1192,7 +1213,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
         }
       }
       // env sums: total collisions += (sum(node) + sum(edge)) // 2  (:239)
-      const int esum = group_sum(has ? (int)node + edge : 0, g.L);
+      const int esum = group_sum(has ? (int)node + edge : 0, LF > 0 ? LF : g.L);
       total += esum / 2;
       rew = rew + g.nc_rew * (double)node;  // :247
       rew = rew + g.ec_rew * (double)edge;  // :249
@@ -1210,7 +1231,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
       PST(6);
       // sum(rewards): naive left fold in agent order (:310)
       if (g.L <= 16) {
-        const double R = row_fold(has ? rew : 0.0, N);
+        const double R = row_fold<LF>(has ? rew : 0.0, N);
         if (ag == 0) {
           if (a.reward) a.reward[env] = R;
           Rsum = R;
@@ -1257,7 +1278,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g, P
     if (a.avail) a.avail[oa] = (uint8_t)am;
   }
   // state (:377-387): [total collisions, step count, sum(each goal cost)]
-  const int gsum = group_sum(has ? gcost : 0, g.L);
+  const int gsum = group_sum(has ? gcost : 0, LF > 0 ? LF : g.L);
   if (env_ok && ag == 0 && a.state) {
     a.state[3 * env + 0] = (float)total;
     a.state[3 * env + 1] = (float)tcur;

@@ -274,9 +274,10 @@ def main():
     # same stream: the same launches again, each recording start / stop events at the
     # kernel's own begin / end (hipExtLaunchKernel, mapfx_rollout_timed) -- the
     # duration rocprofv3 reports for the kernel
-    # (KREP passes of the K steps; the median pass is reported, so one disturbed launch
-    # does not move the roofline)
-    KREP = 5
+    # (KREP passes of the K steps, at least 15 launches in all; the median pass is
+    # reported, so one disturbed launch does not move the roofline, and a rocprofv3 trace
+    # of the command averages enough launches to compare with it)
+    KREP = max(5, -(-15 // nl))
     evs = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             for _ in range(nl)] for _ in range(KREP)]
     for rep_evs in evs:     # torch creates the HIP events at their first record()

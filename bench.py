@@ -523,8 +523,9 @@ def time_gather(dist, b, acts, outs, T, k0, K, world, E, N, keys, payload):
             "rank0_ingress_bytes_per_chunk": ingress,
             "ingress_bound_ms_per_chunk": round(ingress / (max(1, world - 1) * XGMI_LINK_GBS * 1e9)
                                                 * 1e3, 5),
-            "collective": "one torch.distributed.gather (RCCL) per chunk to rank 0 on a side "
-                          "stream, packed %s buffer" % "+".join(keys)}
+            "collective": "one torch.distributed.gather (%s) per chunk to rank 0 on a side "
+                          "stream, packed %s buffer" % ("RCCL" if dist.get_backend() == "nccl"
+                                                        else dist.get_backend(), "+".join(keys))}
 
 
 def payload_arithmetic(T, E, N, W, world):

@@ -536,6 +536,10 @@ __device__ unsigned long long g_stamps[256 * 8];
 #endif
 
 constexpr int FEAT_PRIM = 1, FEAT_FULL = 2;
+// FEAT_RUN (rollouts): exactly the runner output set (reward, term, node, edge, avail,
+// traj_pos / traj_done / traj_t, a window; no reward_f32 / full / PRIMAL), so the
+// per-output tests are compile-time
+constexpr int FEAT_RUN = 4;
 
 // The fp64 reward of one agent from its reward code (deferred fold): bit 0 counted
 // (not done before the step), bit 1 env collision, bit 2 node collision, bits 3.. the
@@ -553,6 +557,7 @@ __device__ inline double code_reward(const Geo& g, uint32_t c) {
 template <typename CellT, int APL, bool ROLL, int FEAT>
 __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   using CT = CellTraits<CellT>;
+  constexpr bool RUNF = (FEAT & FEAT_RUN) != 0;  // exact runner output set (rollouts)
   extern __shared__ __align__(16) unsigned char lds[];
   const int tid = threadIdx.x;
   const int slot = tid >> g.lshift;
@@ -577,7 +582,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   // the last) lanes 0..FR-1 of wave 0 fold one row each -- the same agent-order chain
   // of fp64 adds per step, FR steps' chains side by side -- so the other steps carry no
   // fold and wave 0 writes window records with the others.
-  const int FR = (ROLL && a.do_step) ? g.fold_R : 0;
+  const int FR = (ROLL && (RUNF || a.do_step)) ? g.fold_R : 0;
   uint16_t* codes = (uint16_t*)(lds + g.off_rew);
   double* ctab = (double*)(lds + g.off_ctab);  // code_reward of the codes < 32
   int* bigrow = (int*)(ctab + 32);              // ring row holds a code >= 32 (edge >= 4)
@@ -609,7 +614,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
   const int T = ROLL ? a.T : 1;
   // actions are loaded one step ahead: step s + 1's load is issued before step s's
   // stores, so waiting for it never waits for them (vmcnt counts both, in order)
-  const bool read_act = a.do_step && !a.use_rng;
+  const bool read_act = (RUNF || a.do_step) && !a.use_rng;
   int act_nx[APL];
 #pragma unroll
   for (int k = 0; k < APL; ++k)
@@ -664,7 +669,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       moved[k] = envc[k] = false;
       pre[k] = 0;
       act[k] = 4;
-      if (has[k] && a.do_step) {
+      if (has[k] && (RUNF || a.do_step)) {
         int av;
         if (a.use_rng)
           av = gen_action(a.seed, g.env_offset + env, a.t0 + s, ag);
@@ -696,7 +701,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     lds_barrier();  // B1: every pre-step map read is done (and the bad flag)
     STAMP(1);
     // ================= P1: move the agent counts =================
-    const bool skip = (fl[1] != 0) || !a.do_step;
+    const bool skip = (fl[1] != 0) || !(RUNF || a.do_step);
 #pragma unroll
     for (int k = 0; k < APL; ++k) {
       if (!has[k]) continue;
@@ -713,7 +718,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       }
       if constexpr ((FEAT & FEAT_PRIM) != 0) rcs[ag] = (r[k] << 16) | (c[k] & 0xFFFF);
     }
-    if (a.do_step && !skip && env_ok) ++tcur;
+    if ((RUNF || a.do_step) && !skip && env_ok) ++tcur;
     if (lane == 0) {  // the next step's flags: every read of them (step s - 1's) precedes B1
       int* nf = flag + ((s + 1) & 1) * 4;
       nf[0] = 1;
@@ -731,7 +736,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     int edgek[APL];
 #pragma unroll
     for (int k = 0; k < APL; ++k) edgek[k] = 0;
-    if (g.L >= 64 && a.do_step && !skip) {
+    if (g.L >= 64 && (RUNF || a.do_step) && !skip) {
       // the env's (old, new) cells, 64 agents per chunk, read once by a wave that
       // has such an i; each i's count is then one ballot popcount per chunk
       constexpr int NCH = APL * 4;  // N <= APL * 256
@@ -778,7 +783,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       const int ag = lane + k * g.L;
       const long long ai = (slotE + env) * N + ag;  // output agent index
       int node = 0, edge = edgek[k];
-      if (a.do_step && !skip) {
+      if ((RUNF || a.do_step) && !skip) {
         node = ((uint32_t)map[nc[k]] & CT::CNT) > 1u ? 1 : 0;  // :344-362
         if (g.L < 64 && moved[k] && pre[k] > 0) {
           for (int j = 0; j < N; ++j)
@@ -805,20 +810,20 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         if (tcur >= g.limit) dn[k] = true;                   // :116-117
       } else if (FR) {
         codes[(s & (FR - 1)) * (g.code_pitch >> 1) + ag] = 0;  // code_reward(0) = 0.0
-      } else if (a.do_step) {
+      } else if ((RUNF || a.do_step)) {
         rew[ag] = 0.0;
       }
       if (!dn[k]) fl[0] = 0;  // every writer stores the same 0: no atomic needed
-      if (a.do_step) {
-        if (a.node) a.node[ai] = (uint8_t)node;
-        if (a.edge) {  // u8 while N <= 256 (edge <= N - 1), else u16 (mapfx_edge_elem_size)
+      if ((RUNF || a.do_step)) {
+        if (RUNF || a.node) a.node[ai] = (uint8_t)node;
+        if (RUNF || a.edge) {  // u8 while N <= 256 (edge <= N - 1), else u16 (mapfx_edge_elem_size)
           if (N <= 256) a.edge[ai] = (uint8_t)edge;
           else ((uint16_t*)a.edge)[ai] = (uint16_t)edge;
         }
       }
-      if (a.traj_pos) ((int2*)a.traj_pos)[ai] = make_int2(r[k], c[k]);
-      if (a.traj_done) a.traj_done[ai] = dn[k] ? 1 : 0;
-      if (a.avail) {  // :203-224 on the post-step map
+      if (RUNF || a.traj_pos) ((int2*)a.traj_pos)[ai] = make_int2(r[k], c[k]);
+      if (RUNF || a.traj_done) a.traj_done[ai] = dn[k] ? 1 : 0;
+      if (RUNF || a.avail) {  // :203-224 on the post-step map
         const int cc = nc[k];
         uint32_t m = 16u;
         m |= ((uint32_t)map[cc - g.pitch] != CT::OE) ? 1u : 0u;
@@ -831,7 +836,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     // ---- the env's lane-0 tail: the fp64 fold of the rewards, term, t, next flags ----
     auto lane0_tail = [&](bool alldone) {
       if (!env_ok || lane != 0) return;
-      if (a.do_step) {
+      if ((RUNF || a.do_step)) {
         if (fl[1] && a.err) atomicCAS(a.err, 0, env + 1);
         double R = 0.0;  // `sum(rewards)`: naive left fold in agent order (:141)
         if (!FR) {
@@ -859,12 +864,12 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
           for (; j < N; ++j) R = R + rew[j];
         }
         if (!FR) {
-          if (a.reward) a.reward[slotE + env] = R;
-          if (a.reward_f32) a.reward_f32[slotE + env] = (float)R;
+          if (RUNF || a.reward) a.reward[slotE + env] = R;
+          if (!RUNF && a.reward_f32) a.reward_f32[slotE + env] = (float)R;
         }
       }
-      if (a.term) a.term[slotE + env] = alldone ? 1 : 0;
-      if (a.traj_t) a.traj_t[slotE + env] = tcur;
+      if (RUNF || a.term) a.term[slotE + env] = alldone ? 1 : 0;
+      if (RUNF || a.traj_t) a.traj_t[slotE + env] = tcur;
     };
     STAMP(4);
     // ---- deferred fold: lane i < FR of wave 0 folds the code row of step s0 + i ----
@@ -915,8 +920,8 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       bigrow[tid] = 0;
       for (; j < N; ++j) R = R + val(cs[j]);
       const long long ri = (long long)(s0 + tid) * Elong + env;
-      if (a.reward) a.reward[ri] = R;
-      if (a.reward_f32) a.reward_f32[ri] = (float)R;
+      if (RUNF || a.reward) a.reward[ri] = R;
+      if (!RUNF && a.reward_f32) a.reward_f32[ri] = (float)R;
       if (MAPFX_FOLD_PRIO) __builtin_amdgcn_s_setprio(0);
     };
     // One env per block over four waves (N > 128): wave 0 runs the tail (the fold is
@@ -1061,7 +1066,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
       if (!has[k]) continue;
       const int ag = lane + k * g.L;
       const long long i = (long long)env * N + ag;
-      if (a.autoreset && alldone && a.do_step) {
+      if (a.autoreset && alldone && (RUNF || a.do_step)) {
         const int2 p = ((const int2*)a.init_pos)[i];
         const int ocell = (r[k] + g.P) * g.pitch + c[k] + g.pl;
         const int ncell = (p.x + g.P) * g.pitch + p.y + g.pl;
@@ -1073,7 +1078,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
         st[k] = 0;
       }
     }
-    if (a.autoreset && alldone && a.do_step) tcur = 0;
+    if (a.autoreset && alldone && (RUNF || a.do_step)) tcur = 0;
     // B4: the autoreset's map atomics before the next step's reads; without autoreset
     // every hand-off of this step is already ordered by B3 (the tail and the fold read
     // nothing the next step writes before its B1)
@@ -2419,9 +2424,18 @@ KernelFn pick_kernel_cf(int apl, bool roll) {
   return mapf_step_kernel<CellT, 4, FEAT>;
 }
 
-// feat: 0 (window / avail / rewards), FEAT_FULL, or FEAT_FULL | FEAT_PRIM
+// rollouts with exactly the runner output set
+template <typename CellT>
+KernelFn pick_kernel_run(int apl) {
+  if (apl == 1) return mapf_rollout_kernel<CellT, 1, FEAT_RUN>;
+  if (apl == 2) return mapf_rollout_kernel<CellT, 2, FEAT_RUN>;
+  return mapf_rollout_kernel<CellT, 4, FEAT_RUN>;
+}
+
+// feat: 0 (window / avail / rewards), FEAT_FULL, FEAT_FULL | FEAT_PRIM, or FEAT_RUN (rollouts)
 template <typename CellT>
 KernelFn pick_kernel_c(int apl, bool roll, int feat) {
+  if ((feat & FEAT_RUN) && roll) return pick_kernel_run<CellT>(apl);
   if (feat & FEAT_PRIM) return pick_kernel_cf<CellT, FEAT_FULL | FEAT_PRIM>(apl, roll);
   if (feat & FEAT_FULL) return pick_kernel_cf<CellT, FEAT_FULL>(apl, roll);
   return pick_kernel_cf<CellT, 0>(apl, roll);
@@ -2515,7 +2529,10 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
       return check_hip(hipGetLastError(), "mapf_wave_kernel launch");
     }
   }
-  const int feat = (a.obs_primal || a.primal_vec) ? (FEAT_FULL | FEAT_PRIM) : a.obs_full ? FEAT_FULL : 0;
+  int feat = (a.obs_primal || a.primal_vec) ? (FEAT_FULL | FEAT_PRIM) : a.obs_full ? FEAT_FULL : 0;
+  if (roll && feat == 0 && a.reward && a.term && a.node && a.edge && a.avail && a.traj_pos && a.traj_done &&
+      a.traj_t && (a.obs_window || a.obs_window_occ) && !a.reward_f32)
+    feat = FEAT_RUN;  // the runner output set: the per-output tests compile away
   KernelFn fn = pick_kernel(h->cell_bytes, h->APL, roll, feat);
   const int blocks = (g.E + g.EPB - 1) / g.EPB;
   const int lds = g.gen_lds;
@@ -2825,9 +2842,9 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
   const int lds_total = g.gen_lds;
   if (lds_total > 64 * 1024) {
     hipError_t e = hipSuccess;
-    const int feats[3] = {0, FEAT_FULL, FEAT_FULL | FEAT_PRIM};
+    const int feats[4] = {0, FEAT_FULL, FEAT_FULL | FEAT_PRIM, FEAT_RUN};
     for (int roll = 0; roll < 2 && e == hipSuccess; ++roll)
-      for (int fi = 0; fi < 3 && e == hipSuccess; ++fi)
+      for (int fi = 0; fi < 4 && e == hipSuccess; ++fi)
         e = hipFuncSetAttribute((const void*)pick_kernel(es, h->APL, roll != 0, feats[fi]),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds_total);
     if (e != hipSuccess) {

@@ -90,6 +90,41 @@ def parse():
     return ap.parse_args()
 
 
+ACT_SEED = 2          # the device generator's action seed of every timed leg
+
+
+def mapf_workload(config, window, device, offset=0):
+    """One mapf_grid bench leg's batch and output set: what the timed launches run.
+    tests/test_gpu_parity.py::test_bench_leg_matches_oracle builds its launches from
+    this same function, so the instance a bench line times is the instance the test
+    checks against the oracle."""
+    import mapfx
+    from mapfx.maps import synthetic_instances, warehouse_grid
+    S, N, E, p, shared = CONFIGS[config]
+    inst = synthetic_instances(E, S, S, N, p_obstacle=p or 0.0, seed=1, env_offset=offset,
+                               shared_grid=warehouse_grid(S) if shared else None)
+    limit = 2 ** 31 - 1
+    # N > 127: agent counts need int16 cells; the window leaves as ONE int16 occupancy
+    # plane (obs_window_occ: obstacle = -1, agents = max(v, 0)), 2 B per window cell,
+    # instead of two int16 planes (the 0/1 obstacle plane would pay 2 B per cell)
+    wkind = "window_occ" if N > 127 else "window"
+    wkey = "obs_" + wkind
+    b = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
+                            episode_limit=limit, obs=(wkind,), window=window,
+                            device=device, env_offset=offset, track_steps=False)
+    outs = ("reward", "term", "node", "edge", "avail", wkey, "traj_pos", "traj_done", "traj_t")
+    return {"S": S, "N": N, "E": E, "p": p, "shared": shared, "inst": inst, "batch": b,
+            "wkind": wkind, "wkey": wkey, "outs": outs, "limit": limit}
+
+
+def bench_traj(b, T):
+    """The trajectory buffers of a timed launch: every rollout output but the f32 reward
+    copy (the runner set: the kernel instance without it is the one timed)."""
+    traj = b._alloc_out(T)
+    traj.pop("reward_f32")
+    return traj
+
+
 def out_bytes_per_env_step(N, W):
     """Algorithmic HBM bytes of one env step of the fused rollout:
     actions N (read) + pos 8N + done N + t 4 + reward 8 + term 1 + node N + edge N
@@ -235,23 +270,13 @@ def main():
     n_full, rem = divmod(K, T)              # K = n_full launches of T (+ one of rem)
     n_wu = -(-WU // T) if WU > 0 else 0     # warmup: whole launches of the timed shape
     offset = rank * E                 # weak scaling: rank r owns global envs [r*E, (r+1)*E)
-    inst = synthetic_instances(E, S, S, N, p_obstacle=p or 0.0, seed=1, env_offset=offset,
-                               shared_grid=warehouse_grid(S) if shared else None)
-    limit = 2 ** 31 - 1
-    # N > 127: agent counts need int16 cells; the window leaves as ONE int16 occupancy
-    # plane (obs_window_occ: obstacle = -1, agents = max(v, 0)), 2 B per window cell,
-    # instead of two int16 planes (the 0/1 obstacle plane would pay 2 B per cell)
-    wkind = "window_occ" if N > 127 else "window"
-    wkey = "obs_" + wkind
-    b = mapfx.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
-                            episode_limit=limit, obs=(wkind,), window=W,
-                            device="cuda:%d" % local, env_offset=offset, track_steps=False)
+    wl = mapf_workload(args.config, W, "cuda:%d" % local, offset)
+    inst, b, wkind, wkey, outs, limit = (wl[k] for k in ("inst", "batch", "wkind", "wkey",
+                                                         "outs", "limit"))
     b.reset()
     stream = torch.cuda.current_stream()
-    acts = b.gen_actions(n_wu * T + K, seed=2)                 # inputs resident in HBM
-    traj = b._alloc_out(T)
-    traj.pop("reward_f32")
-    outs = ("reward", "term", "node", "edge", "avail", wkey, "traj_pos", "traj_done", "traj_t")
+    acts = b.gen_actions(n_wu * T + K, seed=ACT_SEED)           # inputs resident in HBM
+    traj = bench_traj(b, T)
 
     def plan(k0, t, events=None):
         tr = traj if t == T else {k: v[:t] for k, v in traj.items()}

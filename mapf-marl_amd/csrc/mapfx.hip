@@ -1627,10 +1627,12 @@ __device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a
       if (a.err && (fl & SF_SKIP)) atomicCAS(a.err, 0, (int)env + 1);
     }
     // the batch ends here: every code of it is in the ring (this wave's b(q) just now,
-    // the other wave's b(q - 1) before the last barrier)
-    if ((q & 15u) == 15u || q + 1 == (uint32_t)T) {
+    // the other wave's b(q - 1) before the last barrier).  Not so for the launch's last
+    // step: b(T - 1) runs in the same interval as the other wave's b(T - 2), so that batch
+    // is folded after one more barrier, below
+    if ((q & 15u) == 15u && q + 1 != (uint32_t)T) {
       wave_fence();
-      fold_batch(q & ~15u, (int)(q & 15u) + 1);
+      fold_batch(q & ~15u, 16);
     }
   };
 
@@ -1658,6 +1660,10 @@ __device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a
       part_b((uint32_t)(q - 1));
     }
   }
+  // barrier T + 1 (the step wave meets it after its state write-back): codes T - 2 (the
+  // other wave's) and T - 1 (this wave's) are both in the ring
+  split_barrier();
+  if (T > 0 && ((T - 1) & 1) == par) fold_batch((uint32_t)(T - 1) & ~15u, ((T - 1) & 15) + 1);
 }
 
 // FULLW: every lane owns an agent (N == L and E % EPW == 0) -> no lane masks.
@@ -2145,6 +2151,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
     a.done[oa] = dn ? 1 : 0;
     if (a.steps) a.steps[oa] = st;
     if (ag == 0) a.t[env] = tcur;
+    split_barrier();  // barrier T + 1: the store waves' last fold (split_store_wave_dbm)
     return;
   }
 

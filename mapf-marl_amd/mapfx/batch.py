@@ -330,12 +330,17 @@ class MapfGridBatch:
         an obstacle cell is legal state (quirk 1: agents may stand on obstacles, e.g.
         transposed .scen starts) and is observed exactly as the reference would.
         Any strided input (a slice of unpack_compact's output) is accepted."""
-        p = torch.as_tensor(pos, device=self.device).to(torch.int32).reshape(self.E, self.N, 2)
-        lo = torch.tensor([0, 0], device=self.device)
-        hi = torch.tensor([self.H, self.W], device=self.device)
-        if p.numel() and not bool(((p >= lo) & (p < hi)).all()):
+        p = torch.as_tensor(pos, device=self.device)
+        if p.dtype.is_floating_point or p.dtype.is_complex or p.dtype == torch.bool:
+            raise TypeError("positions must be an integer tensor, got %s" % p.dtype)
+        p = p.reshape(self.E, self.N, 2)
+        # range check before the int32 cast: an int64 outside int32 must not wrap onto the grid
+        p64 = p.to(torch.int64)
+        lo = torch.tensor([0, 0], device=self.device, dtype=torch.int64)
+        hi = torch.tensor([self.H, self.W], device=self.device, dtype=torch.int64)
+        if p.numel() and not bool(((p64 >= lo) & (p64 < hi)).all()):
             raise ValueError("positions outside the %dx%d grid" % (self.H, self.W))
-        self.pos.copy_(p)
+        self.pos.copy_(p.to(torch.int32))
         if done is not None:
             self.done.copy_(torch.as_tensor(done, device=self.device).reshape(self.E, self.N))
         if t is not None:

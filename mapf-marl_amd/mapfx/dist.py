@@ -184,13 +184,18 @@ class OverlappedGather:
 
     Uneven shards (mapfx.dist.shard of an env count the world does not divide): the
     ranks exchange their env counts once at construction; every rank sends the
-    largest rank's prefix size (its own prefix, then padding), so the collective's
-    equal-size contract holds, and result(i) returns one dict of views per rank, each
-    cut to that rank's env count, instead of [world, ...] views.
+    largest rank's prefix size (its own prefix, then whatever bytes follow it in its
+    chunk buffer -- e.g. its other rollout outputs such as traj_pos; dst ignores them),
+    so the collective's equal-size contract holds, and result(i) returns one dict of
+    views per rank, each cut to that rank's env count, instead of [world, ...] views.
+
+    Construction is COLLECTIVE unless `rank_envs` (every rank's env count, e.g. from
+    mapfx.dist.shard) is given: it runs one all_reduce of the env counts, so every
+    rank of the group must construct its OverlappedGather in the same order.
     """
 
     def __init__(self, batch, T: int, keys=("obs_window", "reward", "traj_done"), outputs=None,
-                 dst: int = 0, group=None, compact=False):
+                 dst: int = 0, group=None, compact=False, rank_envs=None):
         import torch.distributed as dist
         self.dist = dist
         self.batch = batch
@@ -212,11 +217,17 @@ class OverlappedGather:
         self.cuda = torch.device(dev).type == "cuda"
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        # every rank's env count (one small all-reduce at construction)
-        counts = torch.zeros(self.world, dtype=torch.int64, device=dev)
-        counts[self.rank] = int(batch.E)
-        dist.all_reduce(counts, group=group)
-        self.rank_envs = [int(c) for c in counts.tolist()]
+        # every rank's env count (given, or one small all-reduce at construction)
+        if rank_envs is not None:
+            self.rank_envs = [int(c) for c in rank_envs]
+            if len(self.rank_envs) != self.world or self.rank_envs[self.rank] != int(batch.E):
+                raise ValueError("rank_envs %r does not match world %d / this rank's %d envs"
+                                 % (self.rank_envs, self.world, int(batch.E)))
+        else:
+            counts = torch.zeros(self.world, dtype=torch.int64, device=dev)
+            counts[self.rank] = int(batch.E)
+            dist.all_reduce(counts, group=group)
+            self.rank_envs = [int(c) for c in counts.tolist()]
         self.even = len(set(self.rank_envs)) == 1
         # each rank's gathered prefix (its own layout: the env dimension of every
         # gathered [T, E, ...] tensor is that rank's count), whole 16-B units so every

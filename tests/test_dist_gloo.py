@@ -293,7 +293,10 @@ def _og_uneven_worker(rank, world, port, q, n_total, compact):
         inst = synthetic_instances(cnt, c["S"], c["S"], c["N"], p_obstacle=0.1, seed=5, env_offset=off)
         fb = _OracleTrajBatch(inst, c["S"], c["N"], c["W"], off)
         keys = "compact" if compact else ("obs_window_occ", "reward", "traj_done")
-        og = OverlappedGather(fb, c["T"], keys=keys, compact=compact)
+        # compact: the counts handed in from shard() (no construction all_reduce);
+        # otherwise exchanged by the constructor's collective
+        given = [shard(n_total, r, world)[1] for r in range(world)] if compact else None
+        og = OverlappedGather(fb, c["T"], keys=keys, compact=compact, rank_envs=given)
         assert not og.even and og.rank_envs == [shard(n_total, r, world)[1] for r in range(world)]
         got = []
         for i in range(c["chunks"]):

@@ -220,7 +220,9 @@ def test_batched_primal_matches_oracle(mapfx_mod, S, N, s, E):
     (64, 64, 40, 8, ("full", "window"), 5),
     (64, 64, 40, 8, ("full", "window", "primal"), 5),
     (128, 256, 4, 4, ("full", "window", "primal"), 5),
-    (128, 256, 6, 6, ("window_occ",), 5),                  # C5 shape, the bench's outputs
+    # C5 shape with the occupancy window (+ reward_f32 and the full output set: feature
+    # set 0, NOT the bench's FEAT_RUN instance -- that one is test_bench_leg_matches_oracle)
+    (128, 256, 6, 6, ("window_occ",), 5),
     (100, 300, 5, 5, ("window", "window_occ"), 7),          # APL 2
     (32, 16, 300, 12, ("window_occ",), 3)])                 # u8 cells, 16 envs per block
 def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T, obs, win):
@@ -360,48 +362,83 @@ def test_runner_rollout_agents_on_obstacles(mapfx_mod, autoreset):
 C2_SPLIT_INSTANCE = {20: "mapf_wave_kernel<5, true, true, true, 16, true, false, 8>",
                      64: "mapf_wave_kernel<5, true, true, true, 16, true, false, 0>"}
 
+# every timed mapf_grid leg of bench.py: (config, T).  T = 20 is the driver's
+# `--steps 20`, T = 64 the default --chunk; T = 33 is the first C2 launch past the
+# short-action-block threshold.
+BENCH_LEGS = [("c2", 20), ("c2", 64), ("c2", 33), ("c1", 64), ("c1", 20), ("c3", 64),
+              ("c3", 20), ("c5", 64), ("c5", 20)]
 
-@pytest.mark.parametrize("T", [20, 64, 33])
-def test_bench_rollout_matches_oracle_every_step(mapfx_mod, T):
-    """The driver's exact launch (bench.py --steps 20: C2, 4096 envs, int8 actions resident
-    in HBM, the bench's output set, one launch of T = 20) against the C oracle at EVERY
-    step: reward bits, node, edge, avail, term, window, positions, dones and t.  The
-    launch must be the instance the bench times (checked by name); T = 64 is the default
-    bench chunk, T = 33 the first launch past the short-block threshold."""
+
+def _profile_kernel(config, T, E):
+    """The kernel instance profiles/pmc_<config>.json was taken of, when that profile is
+    of this (config, T, E) workload; else None."""
+    import json
+    import os
+    import bench
+    path = os.path.join(bench.REPO, "profiles", "pmc_%s.json" % config)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pm = json.load(f)
+    if pm.get("config") != config or pm.get("T") != T or pm.get("E") != E:
+        return None
+    return bench.kernel_instance(pm.get("kernel", ""))
+
+
+@pytest.mark.parametrize("config,T", BENCH_LEGS, ids=["%s-T%d" % x for x in BENCH_LEGS])
+def test_bench_leg_matches_oracle(mapfx_mod, config, T):
+    """Every timed bench leg, structurally: the batch, output set and trajectory buffers
+    come from bench.mapf_workload / bench.bench_traj -- the code the bench times -- and
+    the launch is the bench's prepared rollout_plan with int8 actions resident in HBM.
+    Against the C oracle at EVERY step, on every env (C1, C2) or an env slice (C3 every
+    2nd, C5 every 8th, plus the last env): reward bits, node, edge, avail, term, the
+    window (the planes of obs_window_occ at C5), positions, dones and t.  The launched
+    instance must be the one the leg's PMC profile names when that profile is of the
+    same workload (config, T, E)."""
     from mapfx import _abi
-    from mapfx.maps import synthetic_instances
+    from mapfx.batch import window_planes
     from oracle import corc
     import bench
-    S, N, E, p, _ = bench.CONFIGS["c2"]
-    inst = synthetic_instances(E, S, S, N, p_obstacle=p, seed=1)
-    b = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], bits=inst["bits"], hw=(S, S),
-                                episode_limit=2 ** 31 - 1, obs=("window",), window=5,
-                                track_steps=False)
-    ob = corc.OracleBatch(inst["bits"], inst["init_pos"], inst["goals"], S, S, limit=2 ** 31 - 1)
+    wl = bench.mapf_workload(config, 5, "cuda:0")
+    b, S, N, E, inst, wkey = (wl[k] for k in ("batch", "S", "N", "E", "inst", "wkey"))
     b.reset()
-    acts = b.gen_actions(T, seed=2)
-    traj = b._alloc_out(T)
-    traj.pop("reward_f32")
-    outs = ("reward", "term", "node", "edge", "avail", "obs_window", "traj_pos", "traj_done", "traj_t")
-    b.rollout_plan(T, actions=acts, traj=traj, outputs=outs, stream=torch.cuda.current_stream())()
+    acts = b.gen_actions(T, seed=bench.ACT_SEED)
+    traj = bench.bench_traj(b, T)
+    b.rollout_plan(T, actions=acts, traj=traj, outputs=wl["outs"],
+                   stream=torch.cuda.current_stream())()
     name = _abi.last_kernel()
-    if T in C2_SPLIT_INSTANCE:
+    if config == "c2" and T in C2_SPLIT_INSTANCE:
         assert C2_SPLIT_INSTANCE[T] in name, name
+    if config == "c5":      # the FEAT_RUN instance (runner output set, no f32 reward)
+        assert "mapf_rollout_kernel<unsigned short, 1, 4>" in name, name
+    prof = _profile_kernel(config, T, E)
+    if prof is not None:
+        assert bench.kernel_instance(name) == prof, (name, prof)
+    stride = {"c3": 2, "c5": 8}.get(config, 1)
+    envs = np.unique(np.append(np.arange(0, E, stride), E - 1))
+    bits = inst["bits"] if inst["bits"].shape[0] == 1 else inst["bits"][envs]
+    ob = corc.OracleBatch(bits, inst["init_pos"][envs], inst["goals"][envs], S, S,
+                          limit=wl["limit"])
     torch.cuda.synchronize()
-    ah = _np(acts).astype(np.int32)
+    ei = torch.from_numpy(envs).cuda()
+    tr = {k: _np(v.index_select(1, ei)) for k, v in traj.items()}
+    if wkey == "obs_window_occ":
+        tr["obs_window"] = _np(window_planes(traj[wkey].index_select(1, ei)))
+    ah = _np(acts).astype(np.int32)[:, envs]
     for k in range(T):
         r = ob.step(ah[k])
         o = ob.observe(window=5, full=False)
-        assert np.array_equal(_u64(_np(traj["reward"][k])), _u64(r["reward"])), k
-        assert np.array_equal(_np(traj["node"][k]), r["node"]), k
-        assert np.array_equal(_np(traj["edge"][k]), r["edge"]), k
-        assert np.array_equal(_np(traj["avail"][k]), o["avail"]), k
-        assert np.array_equal(_np(traj["term"][k]), o["term"]), k
-        assert np.array_equal(_np(traj["obs_window"][k]), o["obs_window"]), k
-        assert np.array_equal(_np(traj["traj_pos"][k]), ob.pos), k
-        assert np.array_equal(_np(traj["traj_done"][k]), ob.done), k
-        assert np.array_equal(_np(traj["traj_t"][k]), ob.t), k
-    assert np.array_equal(_np(b.pos), ob.pos) and np.array_equal(_np(b.t), ob.t)
+        assert np.array_equal(_u64(tr["reward"][k]), _u64(r["reward"])), k
+        assert np.array_equal(tr["node"][k], r["node"]), k
+        assert np.array_equal(tr["edge"][k], r["edge"]), k
+        assert np.array_equal(tr["avail"][k], o["avail"]), k
+        assert np.array_equal(tr["term"][k], o["term"]), k
+        assert np.array_equal(tr["obs_window"][k], o["obs_window"]), k
+        assert np.array_equal(tr["traj_pos"][k], ob.pos), k
+        assert np.array_equal(tr["traj_done"][k], ob.done), k
+        assert np.array_equal(tr["traj_t"][k], ob.t), k
+    assert np.array_equal(_np(b.pos)[envs], ob.pos) and np.array_equal(_np(b.t)[envs], ob.t)
+    assert np.array_equal(_np(b.done)[envs], ob.done)
 
 
 def test_back_to_back_rollout_launches(mapfx_mod):
@@ -922,19 +959,28 @@ def test_rollout_does_not_pin_trajectories(mapfx_mod):
     assert len(b._traj_cache) == n
 
 
-@pytest.mark.parametrize("S,N,E,T,p,obs", [
-    (128, 256, 40, 21, 0.10, ("window_occ",)),  # C5 shape: folds at steps 7, 15, partial ring at 20
-    (24, 256, 24, 19, 0.05, ("window_occ",)),   # dense: stacked agents, edge counts >= 4 (codes >= 32)
-    (64, 300, 8, 10, 0.10, ("window_occ",)),    # APL 2
+@pytest.mark.parametrize("S,N,E,T,p,obs,runset", [
+    (128, 256, 40, 21, 0.10, ("window_occ",), False),  # C5 shape: folds at steps 7, 15, partial ring at 20
+    (24, 256, 24, 19, 0.05, ("window_occ",), False),   # dense: stacked agents, edge counts >= 4 (codes >= 32)
+    (64, 300, 8, 10, 0.10, ("window_occ",), False),    # APL 2
     # the fold placement after B3 (no window writer to overlap it with): no window
     # outputs at L = 256, and a window at L = 128 with one env per block (the map's LDS)
-    (128, 256, 12, 19, 0.10, ()),
-    (128, 256, 12, 19, 0.10, ("full",)),
-    (160, 100, 10, 12, 0.10, ("window_occ",))])
-def test_generic_rollout_every_step(mapfx_mod, S, N, E, T, p, obs):
+    (128, 256, 12, 19, 0.10, (), False),
+    (128, 256, 12, 19, 0.10, ("full",), False),
+    (160, 100, 10, 12, 0.10, ("window_occ",), False),
+    # FEAT_RUN: exactly the runner output set, no f32 reward (the C5 bench leg's
+    # feature set) at APL 1, 2 and 4, and with the two window planes
+    (128, 256, 40, 21, 0.10, ("window_occ",), True),
+    (24, 256, 24, 19, 0.05, ("window_occ",), True),
+    (64, 300, 8, 10, 0.10, ("window_occ",), True),
+    (64, 600, 6, 10, 0.10, ("window_occ",), True),
+    (160, 100, 10, 12, 0.10, ("window",), True)])
+def test_generic_rollout_every_step(mapfx_mod, S, N, E, T, p, obs, runset):
     """Generic-kernel rollouts (one env per block) fold the rewards from per-agent codes
     every 8 steps; every step's outputs must equal single step launches (per-step fold),
-    bit for bit, including an env whose step 9 is skipped for an invalid action."""
+    bit for bit, including an env whose step 9 is skipped for an invalid action.
+    runset: the rollout writes exactly the runner output set (FEAT_RUN instance)."""
+    from mapfx import _abi
     from mapfx.maps import synthetic_instances
     inst = synthetic_instances(E, S, S, N, p_obstacle=p, seed=17)
     kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=2000, obs=obs, window=5)
@@ -945,7 +991,18 @@ def test_generic_rollout_every_step(mapfx_mod, S, N, E, T, p, obs):
     b2.reset()
     acts = b2.gen_actions(T, 5, t0=0).to(torch.int32)
     acts[9, 2, 0] = 7                            # env 2 skips step 9
-    traj = b1.rollout(T, actions=acts)
+    if runset:
+        traj = b1._alloc_out(T)
+        traj.pop("reward_f32")
+        outs = ("reward", "term", "node", "edge", "avail", "obs_" + obs[0], "traj_pos",
+                "traj_done", "traj_t")
+        traj = b1.rollout(T, actions=acts, traj=traj, outputs=outs)
+        apl = b1.info()["agents_per_lane"]
+        apl = apl if apl <= 2 else 4          # the instance an APL of 3 or 4 runs (pick_kernel_run)
+        name = _abi.last_kernel()
+        assert "mapf_rollout_kernel<" in name and ", %d, 4>" % apl in name, (name, apl)
+    else:
+        traj = b1.rollout(T, actions=acts)
     with pytest.raises(AssertionError):
         b1.check_err()
     max_edge = 0
@@ -955,8 +1012,8 @@ def test_generic_rollout_every_step(mapfx_mod, S, N, E, T, p, obs):
             with pytest.raises(AssertionError):
                 b2.check_err()
         for key in ("reward", "reward_f32", "term", "node", "edge", "avail", "obs_window_occ",
-                    "obs_full"):
-            if key not in out:
+                    "obs_window", "obs_full"):
+            if key not in out or key not in traj:
                 continue
             x, y = _np(out[key]), _np(traj[key][k])
             if x.dtype == np.float64:

@@ -35,6 +35,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <utility>
 #include <new>
@@ -2059,43 +2060,82 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
     unsigned char* ering = (unsigned char*)(info + 128);
     int cp0 = cur, cp1 = cur;  // where this lane's agent is counted in M0 / M1
     bool reset_pending = false;
-    for (int s = 0; s < T; ++s) {
-      const bool odd = (s & 1) != 0;
-      unsigned char* mp = odd ? m1 : map;
-      uint32_t* mp32 = (uint32_t*)mp;
-      if (a.autoreset && __ballot(reset_pending)) {
-        // the last step ended these envs' episodes (their agents are back at init_pos,
-        // mapf_gridworld.py:70-83): count them there in this step's map -- intact since
-        // barrier s - 1's readers are done -- and read their neighbours
-        if (reset_pending) {
-          const int cpi = odd ? cp1 : cp0;
-          atomicAdd(&mp32[cpi >> 2], cpi != cur ? 0u - (1u << ((cpi & 3) * 8)) : 0u);
-          atomicAdd(&mp32[cur >> 2], cpi != cur ? 1u << ((cur & 3) * 8) : 0u);
-          if (odd) cp1 = cur; else cp0 = cur;
-        }
-        wave_fence();
-        if (reset_pending)
-          nb = (uint32_t)mp[cur - pitch] | ((uint32_t)mp[cur + pitch] << 8) |
-               ((uint32_t)mp[cur - 1] << 16) | ((uint32_t)mp[cur + 1] << 24);
-        reset_pending = false;
+    // The step body below is instanced per (map parity, autoreset, invalid-action check):
+    // the parity picks M0 / M1 and cp0 / cp1 at compile time, autoreset is one uniform
+    // branch outside the loop, and the per-step ballot for an invalid action (the env
+    // skips the step, :91-92) runs only in an action block that holds one (blk_bad, from
+    // the block's unpack) -- the step wave's chain paces the launch.
+    bool blk_bad = false;
+    const auto unpack_block = [&](int s_) __attribute__((always_inline)) {  // steps s .. s+AB-1, 4 per u32
+      const int s = __builtin_amdgcn_readfirstlane(s_);  // (wave-uniform)
+      int v[AB];
+      if (a.use_rng) {
+#pragma unroll
+        for (int k = 0; k < AB; ++k) v[k] = gen_action(a.seed, g.env_offset + env, a.t0 + s + k, ag);
+      } else {  // the prefetched block; the next one is issued right away
+#pragma unroll
+        for (int k = 0; k < AB; ++k) v[k] = nxt[k];
+        if (s + AB < T) fetch(s + AB);
       }
-      const int act = next_action(s);
+      uint32_t bad = 0;
+#pragma unroll
+      for (int k = 0; k < (AB + 3) / 4; ++k) actpk[k] = 0;
+#pragma unroll
+      for (int k = 0; k < AB; ++k) {
+        uint32_t u = (uint32_t)v[k];
+        if (s + k >= T) u = 4u;
+        if (u > 4u) u = 0xFFu;  // invalid action (the reference asserts, :92)
+        bad |= u;
+        actpk[k >> 2] |= u << (8 * (k & 3));
+      }
+      blk_bad = __builtin_amdgcn_readfirstlane(__ballot((bad & 0x80u) != 0) != 0 ? 1 : 0) != 0;
+    };
+    const auto step = [&](auto odd_c, auto ar_c, auto chk_c, int s) __attribute__((always_inline)) {
+      constexpr bool ODD = decltype(odd_c)::value;  // map s & 1
+      constexpr bool AR = decltype(ar_c)::value;    // autoreset
+      constexpr bool CHK = decltype(chk_c)::value;  // the block holds an invalid action
+      unsigned char* mp = ODD ? m1 : map;
+      uint32_t* mp32 = (uint32_t*)mp;
+      int& cpr = ODD ? cp1 : cp0;
+      if constexpr (AR) {
+        if (__ballot(reset_pending)) {
+          // the last step ended these envs' episodes (their agents are back at init_pos,
+          // mapf_gridworld.py:70-83): count them there in this step's map -- intact since
+          // barrier s - 1's readers are done -- and read their neighbours
+          if (reset_pending) {
+            const int cpi = cpr;
+            atomicAdd(&mp32[cpi >> 2], cpi != cur ? 0u - (1u << ((cpi & 3) * 8)) : 0u);
+            atomicAdd(&mp32[cur >> 2], cpi != cur ? 1u << ((cur & 3) * 8) : 0u);
+            cpr = cur;
+          }
+          wave_fence();
+          if (reset_pending)
+            nb = (uint32_t)mp[cur - pitch] | ((uint32_t)mp[cur + pitch] << 8) |
+                 ((uint32_t)mp[cur - 1] << 16) | ((uint32_t)mp[cur + 1] << 24);
+          reset_pending = false;
+        }
+      }
+      const int act = (int)(actpk[0] & 0xFFu);
+#pragma unroll
+      for (int k = 0; k < (AB + 3) / 4; ++k)  // shift the packed actions down one byte
+        actpk[k] = (k + 1 < (AB + 3) / 4) ? __builtin_amdgcn_alignbit(actpk[k + 1], actpk[k], 8)
+                                          : (actpk[k] >> 8);
       STAMP(0);
       // A: move decision on the pre-step neighbours (:319-342), this map's count moves
       const int oc = cur;
       const bool mv = !dn && (uint32_t)act < 4u;
       const uint32_t v = mv ? ((nb >> ((act & 3) * 8)) & 0xFFu) : 0u;
       const bool envc = mv && (v & 0x7Fu) == 0u;
-      const bool skip = (__ballot(act == 0xFF) & envmask) != 0;
+      const bool skip = CHK && (__ballot(act == 0xFF) & envmask) != 0;
       const bool moved = mv && (v & 0x7Fu) != 0u && !skip;
       int dlt = (act & 2) ? 1 : pitch;
       dlt = (act & 1) ? dlt : -dlt;
       const int nc = moved ? oc + dlt : oc;
       dep[oc] = (unsigned char)(moved ? (uint32_t)act : 0x7Fu);
-      const int cpi = odd ? cp1 : cp0;
+      const int cpi = cpr;
       atomicAdd(&mp32[cpi >> 2], cpi != nc ? 0u - (1u << ((cpi & 3) * 8)) : 0u);
       atomicAdd(&mp32[nc >> 2], cpi != nc ? 1u << ((nc & 3) * 8) : 0u);
-      if (odd) cp1 = nc; else cp0 = nc;
+      cpr = nc;
       cur = nc;
       STAMP(2);
       // B: the new cell's 4 neighbours (the next move decision, avail) and the pre-step
@@ -2109,7 +2149,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
       // 25.2 vs 21.6 us at C2 T = 20, gpurun_out/r04o: kept here)
       if (s > 0) {
         const int e = edge_of();
-        ering[((s - 1) & 1) * 64 + lane64] = (unsigned char)(e > 255 ? 255 : e);
+        ering[(ODD ? 0 : 1) * 64 + lane64] = (unsigned char)(e > 255 ? 255 : e);
       }
       STAMP(3);
       // D: dones, t (:112-117), the step's info word
@@ -2123,7 +2163,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
       const bool alldone = (__ballot(!dn) & envmask) == 0;
       const uint32_t fl = (dn ? SF_DONE : 0u) | (live ? SF_LIVE : 0u) | (dn_old ? SF_DNOLD : 0u) |
                           (envc ? SF_ENVC : 0u) | (skip ? SF_SKIP : 0u) | (alldone ? SF_ALLDONE : 0u);
-      info[(s & 1) * 64 + lane64] = u32x4{(uint32_t)nc, nbn, fl, (uint32_t)tcur};
+      info[(ODD ? 1 : 0) * 64 + lane64] = u32x4{(uint32_t)nc, nbn, fl, (uint32_t)tcur};
       q_oc = oc;
       q_nc = nc;
       q_act = act;
@@ -2135,18 +2175,36 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
         const int e = edge_of();
         ering[2 * 64 + lane64] = (unsigned char)(e > 255 ? 255 : e);
       }
-      if (a.autoreset && alldone) {  // counted at init_pos in the next step's map
-        const int2 p = ((const int2*)a.init_pos)[oa];
-        cur = cell0 + p.x * pitch + p.y;
-        dn = false;
-        st = 0;
-        tcur = 0;
-        reset_pending = true;
+      if constexpr (AR) {
+        if (alldone) {  // counted at init_pos in the next step's map
+          const int2 p = ((const int2*)a.init_pos)[oa];
+          cur = cell0 + p.x * pitch + p.y;
+          dn = false;
+          st = 0;
+          tcur = 0;
+          reset_pending = true;
+        }
       }
       STAMP(4);
       split_barrier();  // info s, map s & 1, edge s - 1 -> store waves
       STAMP(6);
-    }
+    };
+    typedef std::integral_constant<bool, false> F_;
+    typedef std::integral_constant<bool, true> T_;
+    // two steps (maps 0 and 1) per iteration; AB is even, so both lie in one action block
+    const auto run = [&](auto ar_c) __attribute__((always_inline)) {
+      for (int s = 0; s < T; s += 2) {
+        if ((s & (AB - 1)) == 0) unpack_block(s);
+        if (blk_bad) step(F_{}, ar_c, T_{}, s);
+        else step(F_{}, ar_c, F_{}, s);
+        if (s + 1 < T) {
+          if (blk_bad) step(T_{}, ar_c, T_{}, s + 1);
+          else step(T_{}, ar_c, F_{}, s + 1);
+        }
+      }
+    };
+    if (a.autoreset) run(T_{});
+    else run(F_{});
     ((int2*)a.pos)[oa] = cell_rc(cur);
     a.done[oa] = dn ? 1 : 0;
     if (a.steps) a.steps[oa] = st;

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MAPFX_ABI_VERSION 5
+#define MAPFX_ABI_VERSION 6
 
 /* error codes */
 #define MAPFX_OK 0

@@ -57,6 +57,10 @@ typedef struct mapfx_runner_state {
   int32_t B, N, D;
   uint8_t* alive;        /* [B] env not terminated (after the last step)            */
   uint8_t* alive_prev;   /* [B] running before the last step: the stale list        */
+                         /* (mapfx_runner_step with the post pass fused -- every map
+                            the one-wave-per-env-group kernel takes, N <= 64 and sides
+                            <= 256 -- uses the two as A[0] / A[1], A[ts & 1] = running
+                            before step ts; ABI 6)                                   */
   int64_t* bs;           /* [B] ascending indices of alive_prev, padded with bs[0]: the
                             MAC's `bs` (parallel_runner.py:91, :123)                 */
   int32_t* counts;       /* [2] len(bs), number alive                               */
@@ -64,10 +68,12 @@ typedef struct mapfx_runner_state {
   int64_t* ep_length;    /* [B] episode_lengths (:140)                              */
   int64_t* env_steps;    /* [1] env_steps_this_run (:142)                           */
   int8_t* env_actions;   /* [B][N] the actions the env step reads (mapfx_runner_actions) */
-  int32_t* bs_inv;       /* [B] row of env b in bs, -1 when b is not in it: the fused
+  int32_t* bs_inv;       /* [2][B] row of env b in bs, -1 when b is not in it: the fused
                             step (mapfx_runner_step) reads env b's actions from row
-                            bs_inv[b] of the MAC's output and writes its actions rows
-                            there, so no separate actions pass runs (appended in ABI 4) */
+                            bs_inv[ts & 1][b] of the MAC's output and writes its actions
+                            rows there, so no separate actions pass runs (appended in
+                            ABI 4; two parity halves since ABI 6, the first one used by
+                            the unfused forms) */
 } mapfx_runner_state;
 
 /* reset(): every env's observations (from `out` of mapfx_partial_reset) into row
@@ -99,7 +105,11 @@ int mapfx_runner_post(const mapfx_runner_state* rs, const uint8_t* terminated,
  * same launch -- then mapfx_runner_post(rs, st->terminated, out, ...).  When rows->obs
  * is set, the env step writes the observation rows of the envs running before it
  * straight into rows->obs at ts + 1 (out->obs is then not written) and the post kernel
- * copies no observation bytes. */
+ * copies no observation bytes.
+ * One launch (ABI 6) where the env kernel fuses the post pass (mapfx_runner_state
+ * alive): the compaction for the next MAC call is its last workgroup, over A[ts & 1]
+ * (running before step ts), so counts / counts_out = {len(bs), envs running after step
+ * ts - 1}: the running count lags one step more than mapfx_runner_post's. */
 int mapfx_runner_step(mapfx_partial_t* h, const mapfx_partial_state* st, const mapfx_partial_out* out,
                       const mapfx_runner_state* rs, const void* actions, int32_t action_dtype,
                       int64_t row_stride, int32_t ts, int32_t* counts_out,

@@ -47,6 +47,21 @@ typedef struct mapfx_runner_acts {
   long long ep_avail_sb;
   int64_t* ep_filled;
   long long ep_filled_sb;
+  // The `bs` compaction for the NEXT MAC call fused into the same launch (cmp_bs NULL:
+  // not fused; runner.hip runner_compact_kernel then runs after the step).  The alive
+  // flags are double-buffered by step parity: `alive` is A[ts & 1] (running before this
+  // step: read, never written) and `alive_prev` is A[(ts + 1) & 1] (written for every env:
+  // running after this step), so the launch's last workgroup compacts A[ts & 1] -- the
+  // stale list bs(ts + 1) -- while the env workgroups step.  It writes bs, the row map
+  // cmp_bs_inv (bs_inv of the next step's parity), counts {len(bs), len(bs)}, env_steps
+  // += len(bs) and, when not NULL, counts_out.
+  const uint8_t* cmp_alive;
+  int64_t* cmp_bs;
+  int32_t* cmp_bs_inv;
+  int32_t* cmp_counts;
+  int64_t* cmp_env_steps;
+  int32_t* cmp_counts_out;
+  int cmp_B;
 } mapfx_runner_acts;
 // 1 when mapfx_partial_step_runner can take the post pass (mapfx_runner_acts.alive):
 // the one-wave-per-env-group kernel; the workgroup path (N > 64, a side > 256) cannot

@@ -945,8 +945,63 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
 // RUN: the runner's fused actions / post pass and EpisodeBatch observation rows compiled
 // in (false: the plain step, whose code then holds none of the runner's pointers: 2043
 // -> 1747 VALU instructions)
+// The runner's `bs` compaction for the next MAC call (runner.hip runner_compact_kernel's
+// work) as the extra last workgroup of the runner step's launch (mapfx_runner_acts
+// cmp_*): A = cmp_alive (running before this step) is not written by this launch, so the
+// compaction runs beside the env workgroups instead of as a launch after them.
+// Ascending indices of A, padded with the first; per-thread chunks, a shuffle scan per
+// wave and one barrier for the wave totals (blockDim = 64 * wpb, 64 .. 256 threads).
+__device__ __forceinline__ void runner_compact_block(const mapfx_runner_acts& ra, unsigned char* lds) {
+  const int nt = (int)blockDim.x, tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nw = nt >> 6, B = ra.cmp_B;
+  const int chunk = (B + nt - 1) / nt;
+  const int lo = min(B, tid * chunk), hi = min(B, lo + chunk);
+  int c = 0;
+  for (int b = lo; b < hi; ++b) c += ra.cmp_alive[b] ? 1 : 0;
+  int x = c;  // inclusive scan over the wave's lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  int* ws = (int*)lds;
+  if (lane == 63) ws[wv] = x;
+  __syncthreads();
+  int off = 0, total = 0;
+  for (int i = 0; i < nw; ++i) {
+    const int v = ws[i];
+    off += i < wv ? v : 0;
+    total += v;
+  }
+  int o = off + x - c;  // exclusive prefix of this thread's chunk
+  for (int b = lo; b < hi; ++b) {
+    const bool in = ra.cmp_alive[b] != 0;
+    ra.cmp_bs_inv[b] = in ? o : -1;  // where the next MAC call puts env b's row
+    if (in) ra.cmp_bs[o++] = b;
+  }
+  __syncthreads();  // bs[0] written
+  const int64_t first = total > 0 ? ra.cmp_bs[0] : 0;
+  for (int j = total + tid; j < B; j += nt) ra.cmp_bs[j] = first;
+  if (tid == 0) {
+    ra.cmp_counts[0] = total;  // len(bs) = the envs running before this step
+    ra.cmp_counts[1] = total;  // = the envs running after the previous one
+    ra.cmp_env_steps[0] += total;  // the envs this step steps (env_steps_this_run, :142)
+    if (ra.cmp_counts_out) {  // possibly pinned host memory
+      ra.cmp_counts_out[0] = total;
+      ra.cmp_counts_out[1] = total;
+    }
+  }
+}
+
 template <int WIN, int KF, int LF, int GDE = 0, bool RUN = true>
 __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g_, PArgs a) {
+  if constexpr (RUN) {  // the runner's fused compaction: the launch's extra last workgroup
+    if (a.ra.cmp_bs && blockIdx.x == gridDim.x - 1) {
+      extern __shared__ __align__(16) unsigned char lds_cmp[];
+      runner_compact_block(a.ra, lds_cmp);
+      return;
+    }
+  }
   PGeo g = g_;
   if constexpr (LF > 0) {  // the fast instances' lane group and K as constants (launch() picks
     g.L = LF;              // them only for g.L == LF, g.K == KF)
@@ -1321,7 +1376,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g_, 
         if (ra.ep_term) ra.ep_term[(long long)env * ra.ep_term_sb + (long long)ra.ts * ra.ep_term_st] = term ? 1 : 0;
         ra.ep_return[env] = epr0 + Rsum;
         ra.ep_length[env] = epl0 + 1;
-        ra.alive[env] = term ? 0 : 1;
+        if (!ra.cmp_bs) ra.alive[env] = term ? 0 : 1;  // (fused compaction: A_out below)
         if (ra.ep_state) {  // update(pre_transition_data, bs, ts + 1): state, avail, filled
           float* d = ra.ep_state + (long long)env * ra.ep_state_sb;
           d[0] = (float)total;
@@ -1336,7 +1391,9 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g_, 
         for (int k = 0; k < 5; ++k) d[k] = (int32_t)((am >> k) & 1u);
       }
     }
-    if (ag == 0) ra.alive_prev[env] = live0;
+    // alive_prev: the stale list for the separate compaction, or, with the compaction
+    // fused (cmp_bs), A[(ts + 1) & 1] = running after this step, written for every env
+    if (ag == 0) ra.alive_prev[env] = ra.cmp_bs ? (uint8_t)(live0 && !term ? 1 : 0) : live0;
   }
   // ---- observations of the current state (:312-391) ----
   // per-agent feature rows: curr, start, goal, unit vec, norm, node, edge, steps
@@ -1693,7 +1750,8 @@ int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
       case 9: fn = partial_kernel<9, 0, 0>; break;
       default: return perr(MAPFX_EINVAL, "obs_window must be one of 0, 1, 3, 5, 7, 9");
     }
-  const int nblk = (blocks + g.wpb - 1) / g.wpb;
+  // (+ one workgroup for the runner's fused compaction, partial_kernel's last block)
+  const int nblk = (blocks + g.wpb - 1) / g.wpb + (run && a.ra.cmp_bs ? 1 : 0);
   hipLaunchKernelGGL(fn, dim3(nblk), dim3(64 * g.wpb), g.lds * g.wpb, (hipStream_t)stream, g, a);
   mapfx_note_kernel((const void*)fn);
   return check_hip(hipGetLastError(), "partial_kernel launch");

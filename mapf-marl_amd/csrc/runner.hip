@@ -263,7 +263,13 @@ int mapfx_runner_step(mapfx_partial_t* h, const mapfx_partial_state* st, const m
   // bytes
   mapfx_runner_acts ra;
   memset(&ra, 0, sizeof ra);
-  ra.act_row = rs->bs_inv;
+  // the post pass in the env step's write-back too (the one-wave-per-env-group kernel),
+  // and with it the compaction for the next MAC call as the launch's last workgroup:
+  // alive flags and the row map double-buffered by step parity (alive / alive_prev =
+  // A[0] / A[1], bs_inv = [2][B]; A[ts & 1] = running before step ts)
+  const bool fpost = mapfx_partial_fuses_post(h) != 0;
+  const int par = ts & 1;
+  ra.act_row = rs->bs_inv + (fpost ? (int64_t)par * rs->B : 0);
   ra.act_row_stride = row_stride;
   ra.ep_actions = rows->actions;
   ra.ep_actions_sb = rows->actions_sb;
@@ -273,12 +279,18 @@ int mapfx_runner_step(mapfx_partial_t* h, const mapfx_partial_state* st, const m
   ra.ep_onehot_st = rows->onehot_st;
   ra.ts = ts;
   const bool nxt = ts + 1 < rows->max_t;
-  // the post pass in the env step's write-back too (the one-wave-per-env-group kernel):
-  // then only the compaction runs after it
-  const bool fpost = mapfx_partial_fuses_post(h) != 0;
+  uint8_t* const a_in = par ? rs->alive_prev : rs->alive;   // A[ts & 1]
+  uint8_t* const a_out = par ? rs->alive : rs->alive_prev;  // A[(ts + 1) & 1]
   if (fpost) {
-    ra.alive = rs->alive;
-    ra.alive_prev = rs->alive_prev;
+    ra.alive = a_in;
+    ra.alive_prev = a_out;
+    ra.cmp_alive = a_in;
+    ra.cmp_bs = rs->bs;
+    ra.cmp_bs_inv = rs->bs_inv + (int64_t)(par ^ 1) * rs->B;
+    ra.cmp_counts = rs->counts;
+    ra.cmp_env_steps = rs->env_steps;
+    ra.cmp_counts_out = counts_out;
+    ra.cmp_B = rs->B;
     ra.ep_return = rs->ep_return;
     ra.ep_length = rs->ep_length;
     ra.ep_reward = rows->reward;
@@ -296,12 +308,9 @@ int mapfx_runner_step(mapfx_partial_t* h, const mapfx_partial_state* st, const m
   }
   float* obs_row = rows->obs && nxt ? rows->obs + (int64_t)(ts + 1) * rows->obs_st : nullptr;
   if ((rc = mapfx_partial_step_runner(h, st, actions, action_dtype, &ra, out, obs_row, rows->obs_sb,
-                                      rs->alive, stream)))
+                                      fpost ? a_in : rs->alive, stream)))
     return rc;
-  if (fpost) {
-    hipLaunchKernelGGL(runner_compact_kernel, dim3(1), dim3(CT), 0, (hipStream_t)stream, *rs, counts_out);
-    return launch_ok("runner_compact_kernel launch");
-  }
+  if (fpost) return MAPFX_OK;  // (the compaction ran as the launch's last workgroup)
   if (!rows->obs) return mapfx_runner_post(rs, st->terminated, out, ts, counts_out, rows, stream);
   mapfx_episode_rows r2 = *rows;
   r2.obs = nullptr;

@@ -112,7 +112,7 @@ class RState(ctypes.Structure):  # include/mapfx_runner.h mapfx_runner_state
                             "env_steps", "env_actions", "bs_inv")]
 
 
-ABI_VERSION = 5  # include/mapfx.h MAPFX_ABI_VERSION
+ABI_VERSION = 6  # include/mapfx.h MAPFX_ABI_VERSION
 
 
 class MapfxError(RuntimeError):

@@ -9,9 +9,10 @@ runner step is: the MAC's select_actions, then three device launches
 (include/mapfx_runner.h) -- actions rows, the env step, the step's rows straight
 into the EpisodeBatch tensors with the runner's bookkeeping (running envs, the
 MAC's `bs`, returns, lengths, env steps) kept on the device.  No per-step host
-synchronisation: the loop-exit test reads the count of running envs two steps
-late from a pinned ring (the reference stops one MAC call after the last env
-terminated, and that call is exactly the one the lag covers; see `run`).
+synchronisation: the loop-exit test reads the count of running envs from a pinned
+ring, written by the step two launches back (the reference stops one MAC call after
+the last env terminated; the calls the lag adds find no running env and record
+nothing; see `run`).
 
 The EpisodeBatch is whatever `setup` is given (PyMARL passes
 components.episode_buffer.EpisodeBatch); the runner writes its
@@ -120,8 +121,9 @@ class ParallelRunner:
         self._ep_return, self._ep_length = z((B,), torch.float64), z((B,), torch.int64)
         self._env_steps = z((1,), torch.int64)
         self._env_actions = torch.full((B, N), 4, dtype=torch.int8, device=dev)
-        # row of env b in bs (-1: not in it): the fused step reads b's actions there
-        self._bs_inv = torch.full((B,), -1, dtype=torch.int32, device=dev)
+        # row of env b in bs (-1: not in it): the fused step reads b's actions there;
+        # two halves by step parity (the compaction inside step k writes step k + 1's)
+        self._bs_inv = torch.full((2, B), -1, dtype=torch.int32, device=dev)
         self._rs = _abi.RState(B=B, N=N, D=self.env.obs_dim, alive=ptr(self._alive),
                                alive_prev=ptr(self._alive_prev), bs=ptr(self._bs),
                                counts=ptr(self._counts), ep_return=ptr(self._ep_return),
@@ -250,11 +252,15 @@ class ParallelRunner:
 
         Iteration k of the reference calls the MAC (bs = envs running before step
         k - 1), writes the actions rows, then stops if no env is running after step
-        k - 1, else steps and writes the step's rows.  Here iteration k first
-        stops if no env was running after step k - 2 (pinned ring, two iterations
-        old: no wait in the steady state), which is the reference's stop one
-        iteration later; the one step that can run in between finds no running
-        env and writes nothing."""
+        k - 1, else steps and writes the step's rows.  Here iteration k first stops
+        if the ring slot of launch k - 2 says no env is running: with the post pass
+        and the next MAC call's compaction fused into the env step (one launch per
+        step, mapfx_runner_step) that slot counts the envs running after step k - 3,
+        else (the separate post / compaction kernels) after step k - 2 -- two
+        iterations old either way, so no wait in the steady state.  The iterations
+        the lag adds past the reference's last MAC call find no running env (empty
+        `bs`, no action rows, nothing stepped) and write nothing; the loop also ends
+        when the batch has no row k (every env has met its episode limit by then)."""
         self.reset()
         self.mac.init_hidden(batch_size=self.batch_size)
         r, rs, env = self._erows, ctypes.byref(self._rs), self.env
@@ -269,8 +275,9 @@ class ParallelRunner:
         # cost of one host sync per step (the count of the previous step's compaction).
         exact_bs = bool(getattr(self.args, "runner_exact_bs", False))
         k = 0
-        while True:
-            if k >= 2:   # no env running after step k - 2: the reference stopped at k - 1
+        max_t = int(r.max_t)
+        while k < max_t:
+            if k >= 2:   # none running (after step k - 3 fused, k - 2 unfused): stop
                 ev, hc, _ = self._ring[(k - 2) % _RING]
                 ev.synchronize()
                 if int(hc[1]) == 0:

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     exported = set(re.findall(r"\bT (mapfx_\w+)", nm))
     missing = set(declared) - exported
     assert not missing, missing
-    assert mapfx.lib.mapfx_abi_version() == 5
+    assert mapfx.lib.mapfx_abi_version() == 6
     bid = _abi.build_id()
     assert bid.startswith("src=") and " git=" in bid and "unknown" not in bid, bid
 

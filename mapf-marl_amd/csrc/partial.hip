@@ -946,18 +946,38 @@ __global__ void __launch_bounds__(WG_THREADS) partial_wg_kernel(PGeo g, PArgs a)
 // in (false: the plain step, whose code then holds none of the runner's pointers: 2043
 // -> 1747 VALU instructions)
 // The runner's `bs` compaction for the next MAC call (runner.hip runner_compact_kernel's
-// work) as the extra last workgroup of the runner step's launch (mapfx_runner_acts
+// work) as the extra FIRST workgroup of the runner step's launch (mapfx_runner_acts
 // cmp_*): A = cmp_alive (running before this step) is not written by this launch, so the
-// compaction runs beside the env workgroups instead of as a launch after them.
-// Ascending indices of A, padded with the first; per-thread chunks, a shuffle scan per
-// wave and one barrier for the wave totals (blockDim = 64 * wpb, 64 .. 256 threads).
+// compaction runs beside the env workgroups -- dispatched first, it is done long before
+// them -- instead of as a launch after them.  Ascending indices of A, padded with the
+// first; per-thread chunks (up to 32 flags held as a bit set between the count and the
+// write pass, a 16-flag chunk read as one 16-byte load), a shuffle scan per wave and one
+// barrier for the wave totals (blockDim = 64 * wpb, 64 .. 256 threads).
 __device__ __forceinline__ void runner_compact_block(const mapfx_runner_acts& ra, unsigned char* lds) {
   const int nt = (int)blockDim.x, tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nw = nt >> 6, B = ra.cmp_B;
   const int chunk = (B + nt - 1) / nt;
   const int lo = min(B, tid * chunk), hi = min(B, lo + chunk);
+  const bool held = chunk <= 32;
+  uint32_t bits = 0;  // flag b - lo (held chunks)
   int c = 0;
-  for (int b = lo; b < hi; ++b) c += ra.cmp_alive[b] ? 1 : 0;
+  if (held) {
+    if (chunk == 16 && hi - lo == 16 && ((uintptr_t)(ra.cmp_alive + lo) & 15) == 0) {
+      const uint4 w = *(const uint4*)(ra.cmp_alive + lo);
+      const uint32_t ws4[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {  // bit 7 of each byte: byte != 0
+        const uint32_t nz = (((ws4[i] & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | ws4[i]) & 0x80808080u;
+        const uint32_t m = nz >> 7;
+        bits |= ((m | (m >> 7) | (m >> 14) | (m >> 21)) & 0xFu) << (4 * i);
+      }
+    } else {
+      for (int b = lo; b < hi; ++b) bits |= (ra.cmp_alive[b] ? 1u : 0u) << (b - lo);
+    }
+    c = __popc(bits);
+  } else {
+    for (int b = lo; b < hi; ++b) c += ra.cmp_alive[b] ? 1 : 0;
+  }
   int x = c;  // inclusive scan over the wave's lanes
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -975,7 +995,7 @@ __device__ __forceinline__ void runner_compact_block(const mapfx_runner_acts& ra
   }
   int o = off + x - c;  // exclusive prefix of this thread's chunk
   for (int b = lo; b < hi; ++b) {
-    const bool in = ra.cmp_alive[b] != 0;
+    const bool in = held ? ((bits >> (b - lo)) & 1u) != 0 : ra.cmp_alive[b] != 0;
     ra.cmp_bs_inv[b] = in ? o : -1;  // where the next MAC call puts env b's row
     if (in) ra.cmp_bs[o++] = b;
   }
@@ -995,8 +1015,9 @@ __device__ __forceinline__ void runner_compact_block(const mapfx_runner_acts& ra
 
 template <int WIN, int KF, int LF, int GDE = 0, bool RUN = true>
 __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g_, PArgs a) {
-  if constexpr (RUN) {  // the runner's fused compaction: the launch's extra last workgroup
-    if (a.ra.cmp_bs && blockIdx.x == gridDim.x - 1) {
+  int blk = (int)blockIdx.x;
+  if constexpr (RUN) {  // the runner's fused compaction: the launch's extra first workgroup
+    if (a.ra.cmp_bs && blk-- == 0) {
       extern __shared__ __align__(16) unsigned char lds_cmp[];
       runner_compact_block(a.ra, lds_cmp);
       return;
@@ -1011,7 +1032,7 @@ __global__ void __launch_bounds__(64 * PARTIAL_MAX_WPB) partial_kernel(PGeo g_, 
   extern __shared__ __align__(16) unsigned char lds_blk[];
   constexpr int H2 = WIN / 2;
   const int lane64 = threadIdx.x & 63;
-  const int gw = (int)blockIdx.x * g.wpb + (int)(threadIdx.x >> 6);  // this wave's index
+  const int gw = blk * g.wpb + (int)(threadIdx.x >> 6);  // this wave's index
   unsigned char* const lds = lds_blk + (threadIdx.x >> 6) * g.lds;
   const int slot = lane64 >> g.lshift;
   const int ag = lane64 & (g.L - 1);
@@ -1750,7 +1771,7 @@ int launch(mapfx_partial_t* h, PArgs& a, void* stream) {
       case 9: fn = partial_kernel<9, 0, 0>; break;
       default: return perr(MAPFX_EINVAL, "obs_window must be one of 0, 1, 3, 5, 7, 9");
     }
-  // (+ one workgroup for the runner's fused compaction, partial_kernel's last block)
+  // (+ one workgroup for the runner's fused compaction, partial_kernel's first block)
   const int nblk = (blocks + g.wpb - 1) / g.wpb + (run && a.ra.cmp_bs ? 1 : 0);
   hipLaunchKernelGGL(fn, dim3(nblk), dim3(64 * g.wpb), g.lds * g.wpb, (hipStream_t)stream, g, a);
   mapfx_note_kernel((const void*)fn);

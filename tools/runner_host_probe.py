@@ -61,7 +61,7 @@ def main():
         fixed = (env._h, ctypes.byref(env._state), ctypes.byref(env._out), rs)
         step = lib.mapfx_runner_step
         k = 0
-        while True:
+        while k < int(r.max_t):   # (mapfx/runners.py run(): the batch's last row ends it)
             t0 = time.perf_counter()
             if k >= 2:
                 ev, hc, _ = runner._ring[(k - 2) % _RING]

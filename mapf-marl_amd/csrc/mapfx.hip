@@ -1491,7 +1491,9 @@ __device__ __forceinline__ void stage_occ_record(const uint32_t (&R)[(WIN * WIN 
 constexpr int SPLIT_WAVES = 3;               // step wave + two store waves
 constexpr int SPLIT_DBM_INFO = 2 * 64 * 16;  // info words of two steps
 constexpr int SPLIT_DBM_EDGE = 3 * 64;       // edge counts of two steps + the launch's last step
-constexpr int SPLIT_FOLD_LDS = 256 * 8 + 32 * 64;  // reward-code table + 32-step code ring
+// reward-code table + 32-step code ring: u8 codes (edge <= 15: 16 agents per env) and a
+// 256-entry table, or, with 64 agents per env (edge <= 63), u16 codes and 1024 entries
+__host__ __device__ constexpr int split_fold_lds(int L) { return L > 16 ? 1024 * 8 + 32 * 64 * 2 : 256 * 8 + 32 * 64; }
 
 // info.z flag bits
 constexpr uint32_t SF_DONE = 1, SF_LIVE = 2, SF_DNOLD = 4, SF_ENVC = 8, SF_SKIP = 16, SF_ALLDONE = 64;
@@ -1536,13 +1538,19 @@ __device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a
   const int T = a.T;
   const uint32_t E = (uint32_t)g.E, EN = E * (uint32_t)LL;
   const int slot = lane / LL, ag = lane % LL;
+  // reward codes: node | SF_LIVE | SF_DNOLD | SF_ENVC | edge << 4 -- a byte while the edge
+  // count fits 4 bits (16 agents), a u16 for 64 agents (edge <= 63, 1024 table entries)
+  constexpr bool WIDE = LL > 16;
+  constexpr int NCODE = WIDE ? 1024 : 256;
+  typedef typename std::conditional<WIDE, uint16_t, unsigned char>::type code_t;
+  code_t* const cring = (code_t*)codes;
   const uint32_t env = (uint32_t)(env0 + slot), ag0 = (uint32_t)env0 * LL;
   const u32x4* ost = (const u32x4*)__builtin_assume_aligned(own, 16);
   const u32x4* inf = (const u32x4*)__builtin_assume_aligned(info, 16);
   const int pitch = g.pitch, wpr = g.pitch >> 2;
   uint32_t k_nc = 0, k_nb = 0, k_fl = 0, k_t = 0, k_node = 0;  // step q's, kept from a to b
 
-  for (int c = lane + 64 * par; c < 256; c += 128) {  // the code reward table (as the ALT waves)
+  for (int c = lane + 64 * par; c < NCODE; c += 128) {  // the code reward table (as the ALT waves)
     double rr = 0.0;  // exact fp64 op order of the reference
     if (c & SF_LIVE) {
       if (!(c & SF_DNOLD)) {
@@ -1556,15 +1564,30 @@ __device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a
   }
   auto fold_batch = [&](uint32_t q0, int cnt) {  // one (env, step) per lane, agent order
     const int j = lane & 15, e = lane >> 4;
-    if (j < cnt) {
-      const u32x4 cv = *(const u32x4*)__builtin_assume_aligned(codes + ((q0 + j) & 31) * 64 + e * 16, 16);
-      const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w};
-      double v[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = rtab[(cw[i >> 2] >> (8 * (i & 3))) & 0xFFu];
+    if (j < cnt && e < 64 / LL) {
       double R = 0.0;
+      if constexpr (!WIDE) {
+        const u32x4 cv = *(const u32x4*)__builtin_assume_aligned(codes + ((q0 + j) & 31) * 64 + e * 16, 16);
+        const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w};
+        double v[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) R = R + v[i];
+        for (int i = 0; i < 16; ++i) v[i] = rtab[(cw[i >> 2] >> (8 * (i & 3))) & 0xFFu];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) R = R + v[i];
+      } else {  // the env's 64 agents: 8 x 16 bytes of u16 codes, table reads one group ahead
+        const u32x4* cp = (const u32x4*)__builtin_assume_aligned(cring + ((q0 + j) & 31) * 64, 16);
+        double v[8];
+        u32x4 cv = cp[0];
+#pragma unroll
+        for (int g8 = 0; g8 < 8; ++g8) {
+          const uint32_t cw[4] = {cv.x, cv.y, cv.z, cv.w};
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = rtab[(cw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu];
+          if (g8 + 1 < 8) cv = cp[g8 + 1];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) R = R + v[i];
+        }
+      }
       const uint32_t ei = (q0 + j) * E + (uint32_t)env0 + e;
       split_store((__attribute__((address_space(1))) double*)((gbyte*)a.reward + 8u * ei), R);
       if (a.reward_f32) a.reward_f32[ei] = (float)R;
@@ -1604,8 +1627,8 @@ __device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a
     // (the last step's count has its own slot: the step wave writes it while b(T - 3) may
     // still read slot (T - 1) & 1)
     const uint32_t edge = ering[(q + 1 == (uint32_t)T ? 2u : (q & 1)) * 64 + lane];
-    codes[(q & 31) * 64 + lane] =
-        (unsigned char)(k_node | (k_fl & (SF_LIVE | SF_DNOLD | SF_ENVC)) | ((edge & 0xFu) << 4));
+    cring[(q & 31) * 64 + lane] =
+        (code_t)(k_node | (k_fl & (SF_LIVE | SF_DNOLD | SF_ENVC)) | ((edge & (WIDE ? 0x3Fu : 0xFu)) << 4));
     gbyte* rec = (gbyte*)(OCC ? a.obs_window_occ : a.obs_window) + (q * EN + ag0) * (uint32_t)REC;
 #pragma unroll
     for (int k = 0; k < NRC; ++k)
@@ -1707,7 +1730,8 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
   Geo g = g0;
   MAPFX_HOT_APPLY(a, g);
   extern __shared__ __align__(16) unsigned char lds[];
-  static_assert(!SPLIT || (ROLL && FULLW && RUNNER && LL == 16 && WIN > 0), "split: runner rollout, N = 16");
+  static_assert(!SPLIT || (ROLL && FULLW && RUNNER && (LL == 16 || LL == 64) && WIN > 0),
+                "split: runner rollout, N = 16 or 64");
   static_assert(!OCC || SPLIT, "occupancy records: the split's store waves");
   if constexpr (SPLIT) {
     if (threadIdx.x >= 64) {  // the output side of the split
@@ -1735,7 +1759,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
       unsigned char* ownd = eri + SPLIT_DBM_EDGE;
       double* rt = (double*)(ownd + 2 * 64 * RECB);
       split_store_wave_dbm<WIN, LL, OCC>(g, a, lds + g.wv_off_map, m1, inf, eri, ownd + par * 64 * RECB, rt,
-                                         (unsigned char*)(rt + 256), e0, threadIdx.x & 63, par);
+                                         (unsigned char*)(rt + (LL > 16 ? 1024 : 256)), e0, threadIdx.x & 63, par);
       return;
     }
     if (MAPFX_PRIO_STEP) __builtin_amdgcn_s_setprio(MAPFX_PRIO_STEP);
@@ -2126,7 +2150,11 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
       const bool mv = !dn && (uint32_t)act < 4u;
       const uint32_t v = mv ? ((nb >> ((act & 3) * 8)) & 0xFFu) : 0u;
       const bool envc = mv && (v & 0x7Fu) == 0u;
+#ifdef MAPFX_CHK_RT  // (A/B: the invalid-action test as a uniform branch in one body)
+      const bool skip = blk_bad && (__ballot(act == 0xFF) & envmask) != 0;
+#else
       const bool skip = CHK && (__ballot(act == 0xFF) & envmask) != 0;
+#endif
       const bool moved = mv && (v & 0x7Fu) != 0u && !skip;
       int dlt = (act & 2) ? 1 : pitch;
       dlt = (act & 1) ? dlt : -dlt;
@@ -2195,12 +2223,17 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
     const auto run = [&](auto ar_c) __attribute__((always_inline)) {
       for (int s = 0; s < T; s += 2) {
         if ((s & (AB - 1)) == 0) unpack_block(s);
+#ifdef MAPFX_CHK_RT
+        step(F_{}, ar_c, F_{}, s);
+        if (s + 1 < T) step(T_{}, ar_c, F_{}, s + 1);
+#else
         if (blk_bad) step(F_{}, ar_c, T_{}, s);
         else step(F_{}, ar_c, F_{}, s);
         if (s + 1 < T) {
           if (blk_bad) step(T_{}, ar_c, T_{}, s + 1);
           else step(T_{}, ar_c, F_{}, s + 1);
         }
+#endif
       }
     };
     if (a.autoreset) run(T_{});
@@ -2527,6 +2560,9 @@ KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split, bo
       if (roll && runner && split && fullw && L == 16)
         return short_t ? mapf_wave_kernel<WIN, true, true, true, 16, true, true, 8>
                        : mapf_wave_kernel<WIN, true, true, true, 16, true, true>;
+      if (roll && runner && split && fullw && L == 64)
+        return short_t ? mapf_wave_kernel<WIN, true, true, true, 64, true, true, 8>
+                       : mapf_wave_kernel<WIN, true, true, true, 64, true, true>;
     }
     return nullptr;
   }
@@ -2536,6 +2572,9 @@ KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split, bo
         if (split && fullw && L == 16)
           return short_t ? mapf_wave_kernel<WIN, true, true, true, 16, true, false, 8>
                          : mapf_wave_kernel<WIN, true, true, true, 16, true>;
+        if (split && fullw && L == 64)
+          return short_t ? mapf_wave_kernel<WIN, true, true, true, 64, true, false, 8>
+                         : mapf_wave_kernel<WIN, true, true, true, 64, true>;
       }
       if (!fullw) return mapf_wave_kernel<WIN, true, false, true, 0>;
       if (L == 16) return mapf_wave_kernel<WIN, true, true, true, 16>;
@@ -2577,8 +2616,8 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
     // the split's LDS: M1 (the odd steps' maps of the wave's envs), info + edge rings, the
     // two store waves' staged records, the reward-code table and ring
     const int split_lds = g.wv_lds + g.EPW * g.map_env_bytes + SPLIT_DBM_INFO + SPLIT_DBM_EDGE +
-                          2 * 64 * (occ ? g.wlen / 2 : g.wlen) + SPLIT_FOLD_LDS;
-    const bool split = MAPFX_SPLIT && runner && fullw && g.L == 16 && g.wv_split_ok &&
+                          2 * 64 * (occ ? g.wlen / 2 : g.wlen) + split_fold_lds(g.L);
+    const bool split = MAPFX_SPLIT && runner && fullw && (g.L == 16 || g.L == 64) && g.wv_split_ok &&
                        split_lds <= 64 * 1024 && (al16 & 15) == 0;
     KernelFn fn = pick_wave_kernel((a.obs_window || occ) ? g.window : 0, roll, fullw, runner, g.L, split, occ,
                                    roll && a.T <= MAPFX_AB_SHORT_T);
@@ -2900,7 +2939,7 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     g.wv_lds = o;
     // the store-wave split's LDS (after the wave layout; only that kernel allocates it)
     g.wv_off_split = o;
-    g.wv_split_ok = (L == 16 && (c.window == 3 || c.window == 5 || c.window == 7)) ? 1 : 0;
+    g.wv_split_ok = ((L == 16 || L == 64) && (c.window == 3 || c.window == 5 || c.window == 7)) ? 1 : 0;
     g.wave_ok = (o <= 64 * 1024 && pitch < 256 && g.rows * pitch < 65536) ? 1 : 0;
   }
 

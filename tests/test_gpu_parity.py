@@ -411,9 +411,6 @@ def test_bench_leg_matches_oracle(mapfx_mod, config, T):
         assert C2_SPLIT_INSTANCE[T] in name, name
     if config == "c5":      # the FEAT_RUN instance (runner output set, no f32 reward)
         assert "mapf_rollout_kernel<unsigned short, 1, 4>" in name, name
-    prof = _profile_kernel(config, T, E)
-    if prof is not None:
-        assert bench.kernel_instance(name) == prof, (name, prof)
     stride = {"c3": 2, "c5": 8}.get(config, 1)
     envs = np.unique(np.append(np.arange(0, E, stride), E - 1))
     bits = inst["bits"] if inst["bits"].shape[0] == 1 else inst["bits"][envs]
@@ -439,6 +436,10 @@ def test_bench_leg_matches_oracle(mapfx_mod, config, T):
         assert np.array_equal(tr["traj_t"][k], ob.t), k
     assert np.array_equal(_np(b.pos)[envs], ob.pos) and np.array_equal(_np(b.t)[envs], ob.t)
     assert np.array_equal(_np(b.done)[envs], ob.done)
+    # last: the leg's committed profile must be of this instance (re-profile after a change)
+    prof = _profile_kernel(config, T, E)
+    if prof is not None:
+        assert bench.kernel_instance(name) == prof, (name, prof)
 
 
 def test_back_to_back_rollout_launches(mapfx_mod):
@@ -933,6 +934,49 @@ def test_stacked_swap_edge_count_exact(mapfx_mod, N):
     assert np.array_equal(_np(traj["edge"][0]).astype(np.int64), edge)
     # its reward row comes from the deferred fold's codes (edge >= 4: the arithmetic path)
     assert np.array_equal(_u64(_np(traj["reward"][0])), _u64(_np(out["reward"])))
+
+
+def test_split64_stacked_swap_edges(mapfx_mod):
+    """The store-wave split at 64 agents per env (C3's runner rollout): reward codes are
+    u16 there because an edge count reaches N - 1 = 63 (4 bits hold 15).  Two stacks of
+    32 agents swap cells in step 0 (edge = 32 for every agent), then random steps; every
+    output of every step equals single step launches, and the launch is the split
+    instance."""
+    from mapfx import _abi
+    E, S, N, T = 64, 8, 64, 12
+    grid = np.zeros((S, S), np.int8)
+    init = np.zeros((E, N, 2), np.int32)
+    init[:, :32] = (3, 3)
+    init[:, 32:] = (3, 4)
+    goals = np.zeros((E, N, 2), np.int32)
+    goals[:, :, 0] = 7
+    goals[:, :, 1] = np.arange(N) % S
+    kw = dict(grids=np.repeat(grid[None], E, 0), episode_limit=2000, obs=("window",), window=5)
+    b1 = mapfx_mod.MapfGridBatch(init, goals, **kw)
+    b2 = mapfx_mod.MapfGridBatch(init, goals, **kw)
+    b1.reset()
+    b2.reset()
+    acts = b2.gen_actions(T, 41, t0=0)
+    acts[0, :, :32] = 3            # right: (3,3) -> (3,4)
+    acts[0, :, 32:] = 2            # left:  (3,4) -> (3,3)
+    acts[0, 1, :] = 4              # env 1 stays put
+    traj = b1.rollout(T, actions=acts)
+    assert "mapf_wave_kernel<5, true, true, true, 64, true" in _abi.last_kernel(), _abi.last_kernel()
+    for k in range(T):
+        out = b2.step(acts[k])
+        if k == 0:
+            e0 = _np(out["edge"]).astype(np.int64)
+            assert (e0[0] == 32).all() and (e0[1] == 0).all()
+        for key in ("reward", "reward_f32", "term", "node", "edge", "avail", "obs_window"):
+            x, y = _np(out[key]), _np(traj[key][k])
+            if x.dtype == np.float64:
+                assert np.array_equal(_u64(x), _u64(y)), (key, k)
+            else:
+                assert np.array_equal(x, y), (key, k)
+        assert np.array_equal(_np(traj["traj_pos"][k]), _np(b2.pos)), k
+        assert np.array_equal(_np(traj["traj_done"][k]), _np(b2.done)), k
+        assert np.array_equal(_np(traj["traj_t"][k]), _np(b2.t)), k
+    assert np.array_equal(_np(b1.pos), _np(b2.pos))
 
 
 def test_rollout_does_not_pin_trajectories(mapfx_mod):

@@ -117,9 +117,7 @@ struct Geo {
   int wv_fast;                     // build_map_rows_fast applies (W <= 64, pitch % 8 == 0)
   int nblk;                        // grid size of the launch (set in the kernel from its kernargs)
 };
-#ifndef MAPFX_FAST_WPR
-#define MAPFX_FAST_WPR 24  // words per padded row handled by build_map_rows_fast
-#endif
+constexpr int MAPFX_FAST_WPR = 24;  // words per padded row handled by build_map_rows_fast
 
 struct Args {
   int32_t* pos;
@@ -253,21 +251,8 @@ __device__ __forceinline__ __attribute__((unused)) uint32_t lds_addr(const void*
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
-#ifndef MAPFX_FOLD_R
-#define MAPFX_FOLD_R 8  // deferred-fold ring depth of the generic rollout (power of two; 0 = off)
-#endif
-#ifndef MAPFX_EDGE_READLANE
-#define MAPFX_EDGE_READLANE 1  // generic edge scan: the candidate's cells by v_readlane
-#endif
-#ifndef MAPFX_FOLD_PRIO
-#define MAPFX_FOLD_PRIO 3  // s_setprio of the deferred fold's chain (0: none)
-#endif
-#ifndef MAPFX_OCC_GROUPS
-#define MAPFX_OCC_GROUPS 1  // u16 occupancy windows as 8-row groups of 16-byte stores
-#endif
-#ifndef MAPFX_W0_WRITES
-#define MAPFX_W0_WRITES 1  // wave 0 writes window records on the steps without a fold
-#endif
+constexpr int MAPFX_FOLD_R = 8;  // deferred-fold ring depth of the generic rollout (power of two; 0 = off)
+constexpr int MAPFX_FOLD_PRIO = 3;  // s_setprio of the deferred fold's chain (0: none)
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations,
 // not for its global stores (a __syncthreads() drains every outstanding store --
@@ -766,8 +751,8 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
             const int src = __ffsll((unsigned long long)m) - 1;
             m &= m - 1;
             // src is wave-uniform (a ballot bit): v_readlane, not two ds_bpermute round trips
-            const int tn = MAPFX_EDGE_READLANE ? __builtin_amdgcn_readlane(nc[k], src) : __shfl(nc[k], src);
-            const int to = MAPFX_EDGE_READLANE ? __builtin_amdgcn_readlane(oc[k], src) : __shfl(oc[k], src);
+            const int tn = __builtin_amdgcn_readlane(nc[k], src);
+            const int to = __builtin_amdgcn_readlane(oc[k], src);
             int cnt = 0;
 #pragma unroll
             for (int q = 0; q < NCH; ++q)
@@ -930,7 +915,7 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
     // the deferred fold, wave 0 writes records too except on the fold steps.
     // Without a fold in this step the tail waits until after B3 (no B2b).
     const bool ovl = g.L == 256 && (a.obs_window || a.obs_window_occ);
-    const bool tail_early = ovl && (!FR || fstep || !MAPFX_W0_WRITES);
+    const bool tail_early = ovl && (!FR || fstep);
     if (tail_early) {
       lds_barrier();  // B2b: rew[] / codes and the alldone flag complete
       if (tid < 64) {
@@ -957,13 +942,13 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
           done_occ = true;
           // whole 8-row groups as 16-byte stores, the remaining rows one by one
           if (g.window == 5) {
-            const int rows = MAPFX_OCC_GROUPS ? write_occ16_groups<5>(g, lds, newc_blk, dst, nseg, wtid, wnt) : 0;
+            const int rows = write_occ16_groups<5>(g, lds, newc_blk, dst, nseg, wtid, wnt);
             write_occ16_rows<5>(g, lds, newc_blk, dst, nseg, wtid, wnt, rows);
           } else if (g.window == 3) {
-            const int rows = MAPFX_OCC_GROUPS ? write_occ16_groups<3>(g, lds, newc_blk, dst, nseg, wtid, wnt) : 0;
+            const int rows = write_occ16_groups<3>(g, lds, newc_blk, dst, nseg, wtid, wnt);
             write_occ16_rows<3>(g, lds, newc_blk, dst, nseg, wtid, wnt, rows);
           } else if (g.window == 7) {
-            const int rows = MAPFX_OCC_GROUPS ? write_occ16_groups<7>(g, lds, newc_blk, dst, nseg, wtid, wnt) : 0;
+            const int rows = write_occ16_groups<7>(g, lds, newc_blk, dst, nseg, wtid, wnt);
             write_occ16_rows<7>(g, lds, newc_blk, dst, nseg, wtid, wnt, rows);
           } else {
             done_occ = false;
@@ -1115,11 +1100,6 @@ __device__ __forceinline__ void step_body(const Geo& g, const Args& a) {
 //   agent order; the wave writes the staged records with 16-byte stores.
 // Actions for step s+1 are loaded while step s runs.  All offsets are 32-bit.
 // ===========================================================================
-#ifdef MAPFX_CLOCKS
-// Diagnostic build only: per-wave shader-clock / 100 MHz real-time clock at the
-// start and end of the step loop, read back with mapfx_debug_clocks().
-__device__ unsigned long long g_clk[8 * 32768];
-#endif
 
 // Wave-path cell format: one byte per padded cell = (obstacle << 7) | c with
 // c = count + 1 - obstacle (7 bits), so
@@ -1237,11 +1217,8 @@ __device__ inline void build_map_rows_fast(const Geo& g, uint32_t* map32, const 
 // groups: neighbouring groups' small per-step outputs (node / edge / avail / done
 // bytes, rewards) share 128-B lines, which then fill in one L2 instead of leaving
 // two XCDs as partial-line writes.  Identity when the grid is not a multiple of 8.
-#ifndef MAPFX_XCD
-#define MAPFX_XCD 1
-#endif
 __device__ __forceinline__ int xcd_block(int b, int nb) {
-  if (!MAPFX_XCD || (nb & 7) != 0) return b;
+  if ((nb & 7) != 0) return b;
   return (b & 7) * (nb >> 3) + (b >> 3);
 }
 
@@ -1485,9 +1462,6 @@ __device__ __forceinline__ void stage_occ_record(const uint32_t (&R)[(WIN * WIN 
 // Measured alternatives (a 2-wave form, a single image of raw window rows, a 3-slot ring
 // published a barrier late, a MOVE / MAP step side, nontemporal stores) were slower and
 // are gone from the source; their numbers are in DESIGN.md §4.1b.
-#ifndef MAPFX_SPLIT
-#define MAPFX_SPLIT 1  // store-wave split for the N = 16 runner rollout
-#endif
 constexpr int SPLIT_WAVES = 3;               // step wave + two store waves
 constexpr int SPLIT_DBM_INFO = 2 * 64 * 16;  // info words of two steps
 constexpr int SPLIT_DBM_EDGE = 3 * 64;       // edge counts of two steps + the launch's last step
@@ -1712,12 +1686,7 @@ __device__ __forceinline__ void split_store_wave_dbm(const Geo& g, const Args& a
 // issue arbitration against the other blocks' store waves on its SIMD: C2 T = 20
 // 25.0 -> 23.5 us (round 3; with the round-2 single store wave the store side was the
 // long chain and its priority paid instead).
-#ifndef MAPFX_PRIO_STEP
-#define MAPFX_PRIO_STEP 3
-#endif
-#ifndef MAPFX_PRIO_STORE
-#define MAPFX_PRIO_STORE 0
-#endif
+constexpr int MAPFX_PRIO_STEP = 3;
 // ABT: the action block (0: MAPFX_AB); the split kernel has an 8-step instance for short
 // launches (T <= MAPFX_AB_SHORT_T): C2 T = 20 21.1 vs 21.9 us, while at T = 64 the 16-step
 // block stays faster (52.7 vs 57.0 us; tools/gpucmd_r04q.sh)
@@ -1735,7 +1704,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
   static_assert(!OCC || SPLIT, "occupancy records: the split's store waves");
   if constexpr (SPLIT) {
     if (threadIdx.x >= 64) {  // the output side of the split
-      if (MAPFX_PRIO_STORE) __builtin_amdgcn_s_setprio(MAPFX_PRIO_STORE);
       const int e0 = xcd_block(blockIdx.x, g.nblk) * (64 / LL);
       if (g.wv_fast) {  // the store waves build their share of the padded maps (rows
         // ag + 16 w of each env, w = this wave's index: the step wave takes w = 0), then
@@ -1770,9 +1738,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
   constexpr int NX = WIN > 0 ? WIN : 1;
   constexpr bool FIXN = FULLW && LL > 0;   // N == LL known at compile time
   constexpr bool FLAT = RUNNER && FULLW;   // env outputs stored by every lane of the env
-#ifdef MAPFX_CLOCKS
-  const unsigned long long rtk0 = __builtin_amdgcn_s_memrealtime();
-#endif
   PSTAMP(6);
   const int L = LL > 0 ? LL : g.L;
   const int lshift = LL > 0 ? (LL == 64 ? 6 : LL == 32 ? 5 : LL == 16 ? 4 : LL == 8 ? 3 : LL == 4 ? 2 : LL == 2 ? 1 : 0)
@@ -1807,9 +1772,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
   const int T = ROLL ? a.T : 1;
   // Actions are fetched for AB steps at a time: one VMEM wait per block instead of
   // one per step (a wait on a per-step load would also drain the step's stores).
-#ifndef MAPFX_AB
-#define MAPFX_AB 16
-#endif
+constexpr int MAPFX_AB = 16;
   constexpr int AB = ROLL ? (ABT > 0 ? ABT : MAPFX_AB) : 1;
   uint32_t actpk[(AB + 3) / 4];
   // Action blocks from memory are prefetched one block ahead: block 0 is issued
@@ -2038,10 +2001,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
     nb = (uint32_t)map[cur - pitch] | ((uint32_t)map[cur + pitch] << 8) |
          ((uint32_t)map[cur - 1] << 16) | ((uint32_t)map[cur + 1] << 24);
   PSTAMP(3);
-#ifdef MAPFX_CLOCKS
-  const unsigned long long clk0 = __builtin_amdgcn_s_memtime();
-  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
   // the action of step s: blocks of AB steps unpacked from the prefetch, 4 per u32
   const auto next_action = [&](int s) {
     if ((s & (AB - 1)) == 0) {  // actions of steps s .. s+AB-1, packed 4 per u32
@@ -2150,11 +2109,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
       const bool mv = !dn && (uint32_t)act < 4u;
       const uint32_t v = mv ? ((nb >> ((act & 3) * 8)) & 0xFFu) : 0u;
       const bool envc = mv && (v & 0x7Fu) == 0u;
-#ifdef MAPFX_CHK_RT  // (A/B: the invalid-action test as a uniform branch in one body)
-      const bool skip = blk_bad && (__ballot(act == 0xFF) & envmask) != 0;
-#else
       const bool skip = CHK && (__ballot(act == 0xFF) & envmask) != 0;
-#endif
       const bool moved = mv && (v & 0x7Fu) != 0u && !skip;
       int dlt = (act & 2) ? 1 : pitch;
       dlt = (act & 1) ? dlt : -dlt;
@@ -2223,17 +2178,12 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
     const auto run = [&](auto ar_c) __attribute__((always_inline)) {
       for (int s = 0; s < T; s += 2) {
         if ((s & (AB - 1)) == 0) unpack_block(s);
-#ifdef MAPFX_CHK_RT
-        step(F_{}, ar_c, F_{}, s);
-        if (s + 1 < T) step(T_{}, ar_c, F_{}, s + 1);
-#else
         if (blk_bad) step(F_{}, ar_c, T_{}, s);
         else step(F_{}, ar_c, F_{}, s);
         if (s + 1 < T) {
           if (blk_bad) step(T_{}, ar_c, T_{}, s + 1);
           else step(T_{}, ar_c, F_{}, s + 1);
         }
-#endif
       }
     };
     if (a.autoreset) run(T_{});
@@ -2261,10 +2211,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
     const int nc = moved ? oc + dlt : oc;
     if (has) dep[oc] = (unsigned char)(moved ? (uint32_t)act : 0x7Fu);
     {
-#ifndef MAPFX_FULLW_ATOMICS
-#define MAPFX_FULLW_ATOMICS 1
-#endif
-      if (FULLW && MAPFX_FULLW_ATOMICS) {  // branch-free: lanes that stay add 0 to their own cell's word
+      if (FULLW) {  // branch-free: lanes that stay add 0 to their own cell's word
         atomicAdd(&map32[oc >> 2], moved ? 0u - (1u << ((oc & 3) * 8)) : 0u);
         atomicAdd(&map32[nc >> 2], moved ? 1u << ((nc & 3) * 8) : 0u);
       } else if (moved) {
@@ -2386,19 +2333,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
     wave_fence();
     STAMP(6);
   }
-#ifdef MAPFX_CLOCKS
-  {
-    const unsigned long long clk1 = __builtin_amdgcn_s_memtime();
-    const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
-    if (lane64 == 0 && blockIdx.x < 32768) {
-      g_clk[8 * blockIdx.x + 0] = clk0;
-      g_clk[8 * blockIdx.x + 1] = clk1;
-      g_clk[8 * blockIdx.x + 2] = rt0;
-      g_clk[8 * blockIdx.x + 3] = rt1;
-      g_clk[8 * blockIdx.x + 4] = rtk0;
-    }
-  }
-#endif
   // ---- drain the pipeline: heavy part of the last step, the last two tails ----
   if (T > 0) {
     const double Rp = (ROLL && T > 1) ? fold(T & 1) : 0.0;  // step T-2's row
@@ -2419,10 +2353,6 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
 #ifdef MAPFX_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   PSTAMP(5);
-#endif
-#ifdef MAPFX_CLOCKS
-  __builtin_amdgcn_s_waitcnt(0);
-  if (lane64 == 0 && blockIdx.x < 32768) g_clk[8 * blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
 
@@ -2550,9 +2480,7 @@ int check_hip(hipError_t e, const char* what) {
 }
 
 
-#ifndef MAPFX_AB_SHORT_T
-#define MAPFX_AB_SHORT_T 32
-#endif
+constexpr int MAPFX_AB_SHORT_T = 32;
 template <int WIN>
 KernelFn pick_wave_win(bool roll, bool fullw, bool runner, int L, bool split, bool occ, bool short_t) {
   if (occ) {  // obs_window_occ: only the store-wave split writes it on the wave path
@@ -2617,7 +2545,7 @@ int launch(mapfx_t* h, Args& a, bool roll, hipStream_t stream, hipEvent_t ev0 = 
     // two store waves' staged records, the reward-code table and ring
     const int split_lds = g.wv_lds + g.EPW * g.map_env_bytes + SPLIT_DBM_INFO + SPLIT_DBM_EDGE +
                           2 * 64 * (occ ? g.wlen / 2 : g.wlen) + split_fold_lds(g.L);
-    const bool split = MAPFX_SPLIT && runner && fullw && (g.L == 16 || g.L == 64) && g.wv_split_ok &&
+    const bool split = runner && fullw && (g.L == 16 || g.L == 64) && g.wv_split_ok &&
                        split_lds <= 64 * 1024 && (al16 & 15) == 0;
     KernelFn fn = pick_wave_kernel((a.obs_window || occ) ? g.window : 0, roll, fullw, runner, g.L, split, occ,
                                    roll && a.T <= MAPFX_AB_SHORT_T);
@@ -2732,12 +2660,6 @@ const char* mapfx_last_kernel(void) {
 // error hook for the other translation unit of the library (partial.hip)
 int mapfx_internal_error(int code, const char* msg) { return set_error(code, "%s", msg); }
 
-#ifdef MAPFX_CLOCKS
-extern "C" int mapfx_debug_clocks(unsigned long long* host_out) {
-  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_clk), sizeof(unsigned long long) * 8 * 32768) ==
-                 hipSuccess ? 0 : -1;
-}
-#endif
 #ifdef MAPFX_STAMPS
 int mapfx_debug_stamps(unsigned long long* host_out) {
   return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 256 * 8) ==

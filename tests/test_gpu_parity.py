@@ -1073,6 +1073,42 @@ def test_generic_rollout_every_step(mapfx_mod, S, N, E, T, p, obs, runset):
     assert np.array_equal(_np(b1.steps), _np(b2.steps))
 
 
+@pytest.mark.parametrize("dtype", [torch.int8, torch.int32, torch.int64])
+@pytest.mark.parametrize("T", [1, 3, 4, 5, 13])
+def test_generic_rollout_action_blocks(mapfx_mod, dtype, T):
+    """The generic rollout reads int8 / int32 actions GAB = 4 steps per block (dword loads,
+    rows clamped at T - 1; int64 keeps the one-step load): every launch length around the
+    block size, each action dtype, invalid values (7, -1, and 300 / -300 where the dtype
+    holds them) in several envs and steps -- every step's outputs equal single step launches
+    and the error flag is raised as they raise it."""
+    from mapfx.maps import synthetic_instances
+    S, N, E = 24, 100, 10                     # N > 64: the generic kernel, one env per block
+    inst = synthetic_instances(E, S, S, N, p_obstacle=0.1, seed=23)
+    kw = dict(bits=inst["bits"], hw=(S, S), episode_limit=2000, obs=("window_occ",), window=5)
+    b1 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
+    b2 = mapfx_mod.MapfGridBatch(inst["init_pos"], inst["goals"], **kw)
+    b1.reset()
+    b2.reset()
+    acts = b2.gen_actions(T, 9, t0=0).to(dtype)
+    bad = {torch.int8: (7, -1), torch.int32: (7, -1, 300), torch.int64: (7, -1, -300)}[dtype]
+    for i, v in enumerate(bad):
+        acts[min(T - 1, i + 1), (3 * i + 1) % E, (17 * i) % N] = v
+    traj = b1.rollout(T, actions=acts)
+    err1 = int(b1.err.item())
+    for k in range(T):
+        out = b2.step(acts[k])
+        for key in ("reward", "term", "node", "edge", "avail", "obs_window_occ"):
+            x, y = _np(out[key]), _np(traj[key][k])
+            if x.dtype == np.float64:
+                assert np.array_equal(_u64(x), _u64(y)), (key, k)
+            else:
+                assert np.array_equal(x, y), (key, k)
+        assert np.array_equal(_np(traj["traj_pos"][k]), _np(b2.pos)), k
+        assert np.array_equal(_np(traj["traj_t"][k]), _np(b2.t)), k
+    assert err1 != 0 and int(b2.err.item()) != 0
+    assert np.array_equal(_np(b1.pos), _np(b2.pos)) and np.array_equal(_np(b1.t), _np(b2.t))
+
+
 def test_last_kernel_names_the_launched_instance(mapfx_mod):
     """mapfx_last_kernel (ABI 5) names the env kernel each entry point launched, as
     rocprofv3 does: what bench.py records and checks a profile against."""

@@ -107,7 +107,7 @@ int mapfx_runner_post(const mapfx_runner_state* rs, const uint8_t* terminated,
  * straight into rows->obs at ts + 1 (out->obs is then not written) and the post kernel
  * copies no observation bytes.
  * One launch (ABI 6) where the env kernel fuses the post pass (mapfx_runner_state
- * alive): the compaction for the next MAC call is its last workgroup, over A[ts & 1]
+ * alive): the compaction for the next MAC call is its first workgroup, over A[ts & 1]
  * (running before step ts), so counts / counts_out = {len(bs), envs running after step
  * ts - 1}: the running count lags one step more than mapfx_runner_post's. */
 int mapfx_runner_step(mapfx_partial_t* h, const mapfx_partial_state* st, const mapfx_partial_out* out,

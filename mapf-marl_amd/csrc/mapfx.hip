@@ -162,10 +162,12 @@ struct Args {
       const void *hp_act, int32_t *hp_t, uint32_t hp_geo, uint32_t hp_nm
 // ... and what the first loads' addresses need: hp_geo = H | W << 13 | P << 26 |
 // wv_fast << 31 (the bitmap stride follows from H, W: mapfx_map_stride) and hp_nm =
-// grid size | act_dtype << 27 | do_step << 29 | use_rng << 30 | map_shared << 31 (the
-// XCD-aware block order needs the grid size; gridDim comes from the implicit
-// kernargs).  14 dwords: all that kernel-argument preload fills next to the kernarg
-// pointer.
+// grid size | (T >= 16) << 26 | act_dtype << 27 | do_step << 29 | use_rng << 30 |
+// map_shared << 31 (the XCD-aware block order needs the grid size, gridDim comes from
+// the implicit kernargs; a rollout of at least 16 steps fetches its first action block
+// without a clamp to T, and with every env full E = grid size x envs per block, so the
+// first action loads need no kernarg from memory either).  14 dwords: all that
+// kernel-argument preload fills next to the kernarg pointer.
 #define MAPFX_HOT_APPLY(a, g)                                                                \
   (a).pos = hp_pos, (a).goal = hp_goal, (a).done = hp_done, (a).bits = hp_bits,             \
   (a).actions = hp_act, (a).t = hp_t,                                                       \
@@ -173,14 +175,14 @@ struct Args {
   (g).P = (int)((hp_geo >> 26) & 0x1Fu), (g).wv_fast = (int)(hp_geo >> 31),                \
   (g).bits_words = ((g).H * (g).W + 31) >> 5, (g).map_shared = 0,                           \
   (g).map_stride = (hp_nm >> 31) ? 0 : ((((g).H * (g).W + 7) >> 3) + 15) & ~15,            \
-  (g).nblk = (int)(hp_nm & 0x7FFFFFFu), (a).act_dtype = (int)((hp_nm >> 27) & 3u),         \
+  (g).nblk = (int)(hp_nm & 0x3FFFFFFu), (a).act_dtype = (int)((hp_nm >> 27) & 3u),         \
   (a).do_step = (int)((hp_nm >> 29) & 1u), (a).use_rng = (int)((hp_nm >> 30) & 1u)
 #define MAPFX_HOT_ARGS(a, g, nb)                                                             \
   (a).pos, (a).goal, (a).done, (a).bits, (a).actions, (a).t,                                \
       (uint32_t)(g).H | ((uint32_t)(g).W << 13) | ((uint32_t)(g).P << 26) |                 \
           ((uint32_t)(g).wv_fast << 31),                                                    \
-      (uint32_t)(nb) | ((uint32_t)((a).act_dtype & 3) << 27) | ((a).do_step ? 1u << 29 : 0u) | \
-          ((a).use_rng ? 1u << 30 : 0u) | ((g).map_shared ? 1u << 31 : 0u)
+      (uint32_t)(nb) | ((a).T >= 16 ? 1u << 26 : 0u) | ((uint32_t)((a).act_dtype & 3) << 27) |   \
+          ((a).do_step ? 1u << 29 : 0u) | ((a).use_rng ? 1u << 30 : 0u) | ((g).map_shared ? 1u << 31 : 0u)
 
 template <typename CellT>
 struct CellTraits;
@@ -1713,6 +1715,10 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
         uint32_t pf[1][3];
         const int bl = l64 % LL + LL * (threadIdx.x >> 6);
         fast_row_prefetch<1>(g, src, bl, LL * SPLIT_WAVES, pf);
+        __builtin_amdgcn_sched_barrier(0);
+        // (as in the step wave, below; + the step wave's LDS offsets, dead here)
+        asm volatile("" ::"s"(g0.map_words), "s"(a0.do_step), "s"(g0.wv_off_dep), "s"(g0.wv_off_bits),
+                     "s"(g0.wv_off_rew));
         build_map_rows_fast<MAPFX_FAST_WPR, 1>(g, (uint32_t*)(lds + g.wv_off_map + sl * g.map_env_bytes), src,
                                                bl, LL * SPLIT_WAVES, pf,
                                                (uint32_t*)(lds + g.wv_off_split + sl * g.map_env_bytes));
@@ -1754,6 +1760,57 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
   const bool has = FULLW || (env_ok && ag < N);
   const bool do_step = ROLL || a.do_step;
   const uint64_t envmask = (L == 64 ? ~0ull : ((1ull << L) - 1ull)) << base;
+  const uint32_t oa = (uint32_t)(env * N + ag);  // agent index inside one step slot
+  // (every env full: E = grid x EPW, from the preloaded grid size -- the first action
+  // loads wait for no kernarg fetch)
+  const uint32_t EN = FULLW ? (uint32_t)g.nblk * (uint32_t)(EPW * N) : (uint32_t)(g.E * N);
+  const bool t_long = ROLL && ((hp_nm >> 26) & 1u);  // T >= 16 >= AB
+  // Actions are fetched for AB steps at a time: one VMEM wait per block instead of
+  // one per step (a wait on a per-step load would also drain the step's stores).
+  constexpr int MAPFX_AB = 16;
+  constexpr int AB = ROLL ? (ABT > 0 ? ABT : MAPFX_AB) : 1;
+  static_assert(AB <= 16, "t_long: the first action block lies within T >= 16 steps");
+  uint32_t actpk[(AB + 3) / 4];
+  // Action blocks from memory are prefetched one block ahead: block 0 is issued
+  // first of all (its HBM latency overlaps the state loads and the map build; issued
+  // after them, step 0 still waited ~900 cycles for it at C2 T = 20), block b + 1 as
+  // soon as block b is unpacked, so the wait at a block boundary finds it arrived.
+  int nxt[AB];
+  const bool act_mem = do_step && !a.use_rng;
+  // block 0 of an int8 launch of >= 16 steps: no clamp to T (a kernarg from memory)
+  const bool first_early = act_mem && ROLL && t_long && a.act_dtype == MAPFX_I8;
+  if (first_early) {
+    const int8_t* ap = (const int8_t*)a.actions;
+    const uint32_t oc_ = has ? oa : 0u;
+#pragma unroll
+    for (int k = 0; k < AB; ++k) nxt[k] = (ap + (uint32_t)k * EN)[oc_];
+  }
+
+  // bitmap words of this lane's first map rows (fast build): issued next
+  const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared || !env_ok ? 0 : (long long)env * g.map_stride));
+  // (the split kernel's three waves build the rows together: lane ag + 16 w of 48)
+  constexpr int RPF = SPLIT ? 1 : 4;
+  const int bl = ag, bnl = SPLIT ? LL * SPLIT_WAVES : L;
+  uint32_t pfw[RPF][3];
+  if (g.wv_fast) fast_row_prefetch<RPF>(g, bsrc, bl, bnl, pfw);
+  int tcur = env_ok ? a.t[env] : 0;  // (issued first: its pointer is preloaded)
+  int2 p0 = make_int2(0, 0), q0 = make_int2(0, 0);
+  bool dn = false;
+  if (has) {
+    p0 = ((const int2*)a.pos)[oa];
+    q0 = ((const int2*)a.goal)[oa];
+    dn = a.done[oa] != 0;
+  }
+  // The kernargs past the preloaded ones are fetched at entry and nothing above waits
+  // for them (T and E come from the preloaded dwords).  The dead words of their merged
+  // scalar loads stay live up to here, so no register of a load in flight is reused --
+  // and waited for -- before the loads above are issued: per-step kernel 5.05 -> 4.98 us
+  // (tools/r06/gpu_p.sh; fetched after these loads instead, 5.3 us, gpu_o.sh).
+  if constexpr (FULLW && LL > 0) {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::"s"(g0.map_words), "s"(a0.do_step));
+  }
+
   const int pitch = g.pitch;
   const int Wd = g.W;
   const bool want_win = WIN > 0 && (RUNNER || a.obs_window);
@@ -1766,21 +1823,7 @@ __global__ void __launch_bounds__(SPLIT ? 64 * SPLIT_WAVES : 64, SPLIT ? SPLIT_W
   double* rewL = (double*)(lds + g.wv_off_rew);
   const int rew_buf = g.wv_rew_buf / 8;  // doubles per reward buffer
   const int rew_row = g.wv_rew_row;      // doubles per env row
-
-  const uint32_t oa = (uint32_t)(env * N + ag);  // agent index inside one step slot
-  const uint32_t EN = (uint32_t)(g.E * N);
   const int T = ROLL ? a.T : 1;
-  // Actions are fetched for AB steps at a time: one VMEM wait per block instead of
-  // one per step (a wait on a per-step load would also drain the step's stores).
-constexpr int MAPFX_AB = 16;
-  constexpr int AB = ROLL ? (ABT > 0 ? ABT : MAPFX_AB) : 1;
-  uint32_t actpk[(AB + 3) / 4];
-  // Action blocks from memory are prefetched one block ahead: block 0 is issued
-  // first of all (its HBM latency overlaps the state loads and the map build; issued
-  // after them, step 0 still waited ~900 cycles for it at C2 T = 20), block b + 1 as
-  // soon as block b is unpacked, so the wait at a block boundary finds it arrived.
-  int nxt[AB];
-  const bool act_mem = do_step && !a.use_rng;
   const auto fetch = [&](int s0) {
     // s0 is opaque here: the row offsets are formed at the fetch (scalar row offset +
     // the lane's offset) instead of AB address registers stepped every loop iteration
@@ -1797,25 +1840,13 @@ constexpr int MAPFX_AB = 16;
       for (int k = 0; k < AB; ++k) nxt[k] = (ap + (uint32_t)min(sb + k, T - 1) * EN)[oc_];
     }
   };
-  if (act_mem && ROLL) fetch(0);  // (one step: after the state loads -- a non-int8 action is
-                                  // range-checked at its load, which would wait for it here)
-
-  // bitmap words of this lane's first map rows (fast build): issued next
-  const uint32_t* bsrc = (const uint32_t*)(a.bits + (g.map_shared || !env_ok ? 0 : (long long)env * g.map_stride));
-  // (the split kernel's three waves build the rows together: lane ag + 16 w of 48)
-  constexpr int RPF = SPLIT ? 1 : 4;
-  const int bl = ag, bnl = SPLIT ? LL * SPLIT_WAVES : L;
-  uint32_t pfw[RPF][3];
-  if (g.wv_fast) fast_row_prefetch<RPF>(g, bsrc, bl, bnl, pfw);
-  int tcur = env_ok ? a.t[env] : 0;  // (issued first: its pointer is preloaded)
+  if (act_mem && ROLL && !first_early) fetch(0);  // (one step: after the state loads -- a
+                                                  // non-int8 action is range-checked at its
+                                                  // load, which would wait for it here)
   int cur = 0, gcell = -1, st = 0;  // padded cell of the agent / of its goal
-  bool dn = false;
   if (has) {
-    const int2 p = ((const int2*)a.pos)[oa];
-    const int2 q = ((const int2*)a.goal)[oa];
-    dn = a.done[oa] != 0;
-    cur = cell0 + p.x * pitch + p.y;
-    gcell = cell0 + q.x * pitch + q.y;
+    cur = cell0 + p0.x * pitch + p0.y;
+    gcell = cell0 + q0.x * pitch + q0.y;
     if (a.steps) st = a.steps[oa];
   }
   if (act_mem && !ROLL) fetch(0);
@@ -2690,8 +2721,8 @@ int mapfx_create(const mapfx_cfg* cfg, mapfx_t** out_handle) {
     return set_error(MAPFX_EINVAL, "grid %dx%d out of range", c.H, c.W);
   if (c.n_agents < 1 || c.n_agents > 1024)
     return set_error(MAPFX_EINVAL, "n_agents %d not in 1..1024", c.n_agents);
-  if (c.n_envs < 0 || c.n_envs >= (1 << 27))  // the grid size travels in 27 bits (MAPFX_HOT_ARGS)
-    return set_error(MAPFX_EINVAL, "n_envs %d not in 0..2^27-1", c.n_envs);
+  if (c.n_envs < 0 || c.n_envs >= (1 << 26))  // the grid size travels in 26 bits (MAPFX_HOT_ARGS)
+    return set_error(MAPFX_EINVAL, "n_envs %d not in 0..2^26-1", c.n_envs);
   if ((c.obs_mode & MAPFX_OBS_WINDOW) && (c.window < 1 || c.window > 63))
     return set_error(MAPFX_EINVAL, "window %d not in 1..63", c.window);
   if ((c.obs_mode & MAPFX_OBS_PRIMAL) && (c.primal_size < 1 || c.primal_size > 11))

@@ -271,6 +271,9 @@ def test_rollout_equals_repeated_steps(mapfx_mod, S, N, E, T, obs, win):
     (4096, 64, 5, False, 16),   # the bench shape
     (4096, 20, 5, False, 16),   # the driver's shape: T <= 32 takes the 8-step action-block instance
     (256, 1, 5, False, 16), (256, 2, 5, False, 16), (256, 3, 3, False, 16), (252, 17, 7, False, 16),
+    # T = 15 / 16: either side of the preloaded "T >= 16" bit (the first action block
+    # fetched without a clamp to T)
+    (256, 15, 5, False, 16), (256, 16, 5, False, 16), (128, 16, 5, False, 64),
     (64, 40, 5, True, 16),
     (250, 12, 5, False, 12), (130, 9, 3, True, 7), (66, 10, 5, False, 40),  # N < L
     (130, 12, 5, False, 64), (64, 40, 3, True, 64), (40, 9, 7, False, 64),  # 64-agent store wave

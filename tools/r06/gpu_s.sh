@@ -11,3 +11,6 @@ for rep in 1 2 3; do
   timeout -k 10 300 python3 bench.py --env runner > $O/runner_$rep.json 2> $O/runner_$rep.err || { tail $O/runner_$rep.err; exit 1; }
   python3 -c "import json; d=json.load(open('$O/runner_$rep.json')); print('runner', $rep, d['value'], d['ms_per_step'])"
 done
+# the T = 15 / 16 boundary cases of the split parity test
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "runner_rollout_every_step" > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
+tail -2 $O/tests.txt

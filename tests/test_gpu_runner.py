@@ -90,20 +90,30 @@ def _make_runner(tmp_path, fx, B, mac, **extra):
 def test_runner_matches_reference_parallel_runner(tmp_path, name, fused):
     """fused=False: the runner state without bs_inv (a binding that predates ABI 4), so
     mapfx_runner_step takes the separate actions / env step / post kernels instead of
-    the fused env step; both must fill the batch exactly as the reference runner."""
+    the fused env step; both must fill the batch exactly as the reference runner.
+    Every batch run() returned must still hold its run's rows after the later runs."""
     from conftest import load_fixture
     fx = load_fixture(name)
     runner, logger = _make_runner(tmp_path, fx, int(fx["B"]), ScriptedMAC())
     if not fused:
         runner._rs.bs_inv = None
-    for r in range(int(fx["runs"])):
-        batch = runner.run(test_mode=False)
+
+    def check(r, batch):
         for k, v in batch.data.transition_data.items():
             ref = fx["run%d_%s" % (r, k)]
             got = v.cpu().numpy()
             assert got.shape == ref.shape and got.dtype == ref.dtype, (r, k)
             assert np.array_equal(got.view(np.uint8), ref.view(np.uint8)), (r, k)
+
+    batches = []
+    for r in range(int(fx["runs"])):
+        batch = runner.run(test_mode=False)
+        check(r, batch)
+        batches.append(batch)
         assert runner.t_env == int(fx["run%d_t_env" % r])
+    assert len({b.data.transition_data["obs"].data_ptr() for b in batches}) == len(batches)
+    for r, batch in enumerate(batches):
+        check(r, batch)
     assert [k for k, _, _ in logger.stats] == fx["log_stats"].tolist()
     assert [v for _, v, _ in logger.stats] == fx["log_values"].tolist()
     assert [t for _, _, t in logger.stats] == fx["log_t"].tolist()

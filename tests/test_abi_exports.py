@@ -95,3 +95,27 @@ def test_bits_roundtrip():
     assert np.array_equal(unpack_bits(pack_bits(g), 13, 7), g)
     w = warehouse_grid(64)
     assert w.shape == (64, 64) and (w[0] == -1).all() and 0.3 < (w != 0).mean() < 0.6
+
+
+def test_create_rejects_out_of_range_configs():
+    """mapfx_create validates its configuration before any HIP call (no GPU needed):
+    the grid size of a launch travels in 26 bits of a preloaded kernel argument
+    (MAPFX_HOT_ARGS), so n_envs is limited to 2^26 - 1 envs per handle."""
+    import ctypes
+    from mapfx import lib
+    from mapfx._abi import Cfg
+
+    def create(**kw):
+        c = Cfg(H=8, W=8, n_agents=2, n_envs=4, env_offset=0, episode_limit=100,
+                step_reward=-0.01, collide_reward=-10.0, obs_mode=0, window=5,
+                primal_size=5, map_shared=0)
+        for k, v in kw.items():
+            setattr(c, k, v)
+        h = ctypes.c_void_p()
+        return lib.mapfx_create(ctypes.byref(c), ctypes.byref(h)), lib.mapfx_last_error()
+
+    for kw, what in (({"n_envs": 1 << 26}, b"n_envs"), ({"n_envs": -1}, b"n_envs"),
+                     ({"n_agents": 0}, b"n_agents"), ({"n_agents": 1025}, b"n_agents"),
+                     ({"H": 0}, b"grid"), ({"W": 4097}, b"grid")):
+        rc, msg = create(**kw)
+        assert rc == -1 and what in msg, (kw, rc, msg)
